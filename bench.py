@@ -1,0 +1,178 @@
+"""Benchmark of the MI355X render path on BASELINE.json's headline config.
+
+metric: Mrays/sec (+ frames/sec) at 1920x1080, spp=64, depth 8, on the ~486-
+sphere "Ray Tracing in One Weekend" scene (BASELINE.json configs[1]; scene
+from tools/scenes.py, synthetic and deterministic).  A step = one full frame:
+every pixel sample traced and resolved to RGBA8 in HBM (and, for N>1 GPUs,
+the row tiles gathered over RCCL).  The scene is uploaded before timing.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c5]
+  torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU)
+
+Rank 0 prints one JSON line.  `roofline` prices the trace kernel against the
+FP32 vector peak (the path is VALU-bound), `cpu_baseline`
+times the CPU oracle (the reference's serial-RNG semantics, 1 thread) on a
+bounded row-cyclic sample of the same frame.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+for _p in ("rust-swift-raytracer_amd", "tools"):
+    sys.path.insert(0, os.path.join(ROOT, _p))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+import raytracer_amd as R  # noqa: E402
+import scenes as S  # noqa: E402
+
+METRIC = "Mrays/sec + frames/sec at 1920×1080 spp=64; 1/2/4/8 MI355X"
+FP32_VECTOR_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md, chip-level parameters
+HBM_PEAK_GBS = 8000.0
+ROW_BLOCK = 8  # multi-GPU: row-cyclic blocks of 8 image rows
+
+
+def algorithmic_flops(st):
+    """17*sphere_tests + 14*tri_tests + 60*tri_in_range
+    + 40*rays + 20*samples (no FMA: every add/mul/div/sqrt/compare is 1)."""
+    return (17 * st["sphere_tests"] + 14 * st["tri_tests"] + 60 * st["tri_in_range"]
+            + 40 * st["rays"] + 20 * st["samples"])
+
+
+def cpu_baseline(src, W, H, spp, depth, budget_s):
+    """Oracle (reference serial-RNG semantics), 1 thread, row-cyclic sample."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+
+    scene = O.Scene(src)
+    img = np.zeros((H, W, 4), np.uint8)
+    # calibrate on one mid-frame row, then spread the budget over the frame
+    t = time.perf_counter()
+    _, st, _ = scene.render(W, H, spp, depth, mode=O.RNG_SERIAL, row_begin=H // 3, row_step=H,
+                            out=img)
+    per_row = max(time.perf_counter() - t, 1e-3)
+    nrows = int(max(1, min(H, budget_s / per_row)))
+    step = max(1, H // nrows)
+    t = time.perf_counter()
+    _, st, _ = scene.render(W, H, spp, depth, mode=O.RNG_SERIAL, row_begin=step // 2,
+                            row_step=step, out=img)
+    dt = time.perf_counter() - t
+    return {"value": st["rays"] / dt / 1e6, "unit": "Mrays/s", "cores": 1, "kind": "port",
+            "sample": f"oracle SERIAL RNG, rows {step // 2}::{step} of {W}x{H} "
+                      f"({st['samples']} samples, {st['rays']} rays, {dt:.1f} s)",
+            "msamples_per_s": st["samples"] / dt / 1e6}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--config", default="c2", choices=sorted(S.CONFIGS))
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world_size = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local_rank)
+    if world_size > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+
+    make_scene, W, H, spp, depth = S.CONFIGS[args.config]
+    src = make_scene()
+    world = R.World(src)
+    nr = world_size
+    rows = R.tile_rows(H, ROW_BLOCK, rank, nr) if nr > 1 else H
+    max_rows = max(R.tile_rows(H, ROW_BLOCK, r, nr) for r in range(nr)) if nr > 1 else H
+    dev = torch.device("cuda", local_rank)
+    tile = torch.zeros(max_rows * W * 4, dtype=torch.uint8, device=dev)
+    gathered = torch.empty(nr * max_rows * W * 4, dtype=torch.uint8, device=dev) if nr > 1 else None
+    stream = torch.cuda.current_stream(dev)
+
+    def step():
+        st = world.render_device(W, H, tile.data_ptr(), stream.cuda_stream, spp=spp, depth=depth,
+                                 row_block=ROW_BLOCK, rank=rank, nranks=nr, device=local_rank)
+        if nr > 1:
+            dist.all_gather_into_tensor(gathered, tile)  # RCCL over xGMI
+        return st
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if nr > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    stats = [step() for _ in range(args.steps)]
+    torch.cuda.synchronize()
+    if nr > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+
+    rays = sum(s["rays"] for s in stats)
+    trace_ms = sum(s["trace_ms"] for s in stats) / max(1, sum(s["trace_launches"] for s in stats))
+    if nr > 1:
+        t = torch.tensor([elapsed, float(rays)], dtype=torch.float64, device=dev)
+        dist.all_reduce(t[:1], op=dist.ReduceOp.MAX)
+        dist.all_reduce(t[1:], op=dist.ReduceOp.SUM)
+        elapsed, rays = float(t[0]), int(t[1])
+    if rank != 0:
+        dist.destroy_process_group()
+        return
+
+    st0 = stats[-1]
+    launches = max(1, st0["trace_launches"])
+    flops_per_launch = algorithmic_flops(st0) / launches
+    achieved_tflops = flops_per_launch / (trace_ms * 1e-3) / 1e12
+    out_bytes = rows * W * 4
+    traffic = None
+    tfile = os.path.join(ROOT, "profiles", "hbm_traffic.json")
+    if os.path.exists(tfile):
+        with open(tfile) as fh:
+            traffic = json.load(fh).get(args.config, {}).get("trace_bytes_per_launch")
+    ms_per_step = elapsed / args.steps * 1e3
+    result = {
+        "metric": METRIC,
+        "value": rays / elapsed / 1e6,
+        "unit": "Mrays/s",
+        "n_gpus": nr,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": ms_per_step,
+        "frames_per_sec": 1e3 / ms_per_step,
+        "msamples_per_sec": W * H * spp * args.steps / elapsed / 1e6,
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (deterministic RTOW scene, tools/scenes.py)",
+        "config": {"workload": f"{args.config}: {W}x{H}, spp {spp}, depth {depth}, "
+                               f"{world.num_spheres} spheres, {world.num_triangles} triangles, "
+                               "COUNTER RNG", "width": W, "height": H, "spp": spp,
+                   "depth": depth, "parallelism": f"row-tiles x{nr} (block {ROW_BLOCK})"},
+        "roofline": {"bound": "valu", "achieved": achieved_tflops,
+                     "peak": FP32_VECTOR_PEAK_TFLOPS, "unit": "TFLOP/s",
+                     "frac": achieved_tflops / FP32_VECTOR_PEAK_TFLOPS, "traffic": traffic,
+                     "kernel": "trace_kernel", "avg_launch_ms": trace_ms,
+                     "flops_per_launch": flops_per_launch,
+                     "algorithmic_hbm_gbs": out_bytes / (trace_ms * 1e-3) / 1e9,
+                     "hbm_peak_gbs": HBM_PEAK_GBS},
+        "rays_per_frame": st0["rays"],
+    }
+    if nr == 1 and not args.no_cpu_baseline:
+        result["cpu_baseline"] = cpu_baseline(src, W, H, spp, depth, args.cpu_seconds)
+    print(json.dumps(result))
+    if nr > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,88 @@
+/*
+ * c_raytracer.c -- C twin of the reference caller examples/c_raytracer.rs
+ * (Naxaes/Rust-Swift-Raytracer examples/c_raytracer.rs:48-62): load a world
+ * through load_world, render a 200x200 frame through render (16 spp, depth 8,
+ * lib.rs:51) and write it as an ASCII PPM (image.rs:59-81 format).
+ * Uses only the reference ABI (include/raytracer.h).
+ *
+ * usage: c_raytracer [out.ppm] [scene.txt] [width height]
+ */
+#include <stdio.h>
+#include <stdlib.h>
+
+#include "raytracer.h"
+
+/* The inline world of examples/c_raytracer.rs:15-44 (8 spheres, 2 triangles). */
+static const char *WORLD_SOURCE =
+    "camera origin 0.0 0.0 0.0 aspect 1.77778;\n"
+    "\n"
+    "material RED_DIFFUSE     : Diffuse color 1.0 0.0 0.0;\n"
+    "material GREEN_DIFFUSE   : Diffuse color 0.0 1.0 0.0;\n"
+    "material BLUE_DIFFUSE    : Diffuse color 0.0 0.0 1.0;\n"
+    "material GROUND_MATERIAL : Diffuse color 0.8 0.8 0.0;\n"
+    "material BALL_MATERIAL   : Diffuse color 0.7 0.3 0.3;\n"
+    "\n"
+    "material METAL_MATERIAL_1 : Metal color 0.8 0.8 0.8 fuzz 0.3;\n"
+    "material METAL_MATERIAL_2 : Metal color 0.8 0.6 0.2 fuzz 1.0;\n"
+    "\n"
+    "material MIRROR : Metal color 0.9 0.9 0.9 fuzz 0.0;\n"
+    "material GLASS  : Dielectric ir 1.5;\n"
+    "\n"
+    "sphere center  0.0 -100.5 -1.0  radius 100.0 material GROUND_MATERIAL;\n"
+    "\n"
+    "sphere center  0.0  0.0  -1.0  radius 0.5   material BALL_MATERIAL;\n"
+    "sphere center -1.0  0.0  -1.0  radius 0.5   material METAL_MATERIAL_1;\n"
+    "sphere center  1.0  0.0  -1.0  radius 0.5   material GLASS;\n"
+    "\n"
+    "sphere center  0.0  1.0  -2.0  radius 0.5   material MIRROR;\n"
+    "\n"
+    "sphere center -3.0  2.0  -3.0  radius 0.5   material RED_DIFFUSE;\n"
+    "sphere center  0.0  2.0  -3.0  radius 0.5   material GREEN_DIFFUSE;\n"
+    "sphere center  3.0  2.0  -3.0  radius 0.5   material BLUE_DIFFUSE;\n"
+    "\n"
+    "triangle v0 -0.1 -0.1 -0.5  v1 0.1 -0.1 -0.5  v2 -0.1 0.1 -0.5  material RED_DIFFUSE;\n"
+    "triangle v0 -0.1  0.1 -0.5  v1 0.1 -0.1 -0.5  v2  0.1 0.1 -0.5  material GREEN_DIFFUSE;\n";
+
+static char *read_file(const char *path) {
+    FILE *f = fopen(path, "rb");
+    if (!f) return NULL;
+    fseek(f, 0, SEEK_END);
+    long n = ftell(f);
+    fseek(f, 0, SEEK_SET);
+    char *buf = malloc((size_t)n + 1);
+    if (buf && fread(buf, 1, (size_t)n, f) != (size_t)n) { free(buf); buf = NULL; }
+    if (buf) buf[n] = '\0';
+    fclose(f);
+    return buf;
+}
+
+/* image.rs:59-81 */
+static int write_image(const Rust_CFramebuffer *fb, const char *path) {
+    FILE *f = fopen(path, "w");
+    if (!f) return -1;
+    fprintf(f, "P3\n%zu %zu\n255\n", fb->width, fb->height);
+    for (size_t i = 0; i < fb->width * fb->height; ++i)
+        fprintf(f, "%u %u %u\n", fb->pixels[i].r, fb->pixels[i].g, fb->pixels[i].b);
+    return fclose(f);
+}
+
+int main(int argc, char **argv) {
+    const char *out = argc > 1 ? argv[1] : "examples/image.ppm";
+    char *scene = argc > 2 ? read_file(argv[2]) : NULL;
+    size_t width = argc > 4 ? (size_t)atol(argv[3]) : 200;
+    size_t height = argc > 4 ? (size_t)atol(argv[4]) : 200;
+    if (argc > 2 && !scene) { fprintf(stderr, "cannot read %s\n", argv[2]); return 1; }
+
+    Rust_ColorU8 *pixels = calloc(width * height, sizeof(Rust_ColorU8));
+    Rust_WorldHandle *world = load_world(scene ? scene : WORLD_SOURCE);
+    if (!world) { fprintf(stderr, "load_world failed\n"); return 1; }
+
+    Rust_CFramebuffer fb = {width, height, pixels};
+    Rust_CFramebuffer result = render(fb, world);
+    if (!result.pixels) return 2;
+    if (write_image(&result, out) != 0) { fprintf(stderr, "cannot write %s\n", out); return 3; }
+    printf("wrote %s (%zux%zu)\n", out, result.width, result.height);
+    free(pixels);
+    free(scene);
+    return 0;
+}

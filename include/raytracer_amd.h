@@ -1,0 +1,113 @@
+/*
+ * raytracer_amd.h -- extensions of the MI355X raytracer library beyond the
+ * reference C-ABI (raytracer.h).  Nothing here changes the reference entry
+ * points; it exposes what the reference hard-codes (Options, common.rs:288-317,
+ * fixed to 16 spp / 8 bounces at lib.rs:51), device-resident rendering for
+ * benchmarks, row tiles for multi-GPU, scene introspection and PPM output.
+ */
+#ifndef RAYTRACER_AMD_H
+#define RAYTRACER_AMD_H
+
+#include "raytracer.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* RNG modes.  The reference draws every sample from ONE xorshift32 stream
+ * seeded 2547549 for the whole frame (common.rs:321, random.rs:8-10), which
+ * is a sequential dependency.  The GPU offers:
+ *   RT_RNG_COUNTER: sample (pixel p, index s) starts xorshift32 from
+ *     rt_sample_seed(seed, p*spp + s); draws inside a sample follow the
+ *     reference order exactly.  Default.
+ *   RT_RNG_REPLAY: sample start states are read from a table (e.g. recorded
+ *     from a serial CPU run), which reproduces the serial frame bit-for-bit. */
+enum { RT_RNG_COUNTER = 1, RT_RNG_REPLAY = 2 };
+
+typedef struct RtRenderOptions {
+  int32_t samples_per_pixel;      /* Options.samples_per_pixel (common.rs:290) */
+  int32_t max_ray_bounces;        /* Options.max_ray_bounces   (common.rs:291) */
+  uint32_t rng_mode;              /* RT_RNG_*                                   */
+  uint32_t seed;                  /* COUNTER base seed (default 2547549)        */
+  const uint32_t *replay_states;  /* REPLAY: host table, width*height*spp u32,
+                                     index (row*width + col)*spp + s, row 0 =
+                                     bottom (common.rs:327-336 loop order)      */
+  uint32_t row_block;             /* multi-GPU tile: image rows are dealt in    */
+  uint32_t rank;                  /* blocks of row_block rows, round-robin over */
+  uint32_t nranks;                /* nranks; this call renders rank's rows      */
+  int32_t device;                 /* HIP device ordinal, -1 = current device    */
+} RtRenderOptions;
+
+typedef struct RtRenderStats {
+  uint64_t samples;        /* pixel samples traced                           */
+  uint64_t rays;           /* World::hit calls (primary + bounces)           */
+  uint64_t sphere_tests;   /* rays * spheres (brute force, common.rs:241)     */
+  uint64_t tri_tests;      /* rays * triangles (common.rs:182)               */
+  uint64_t tri_in_range;   /* triangle tests that passed the t-range check   */
+  double trace_ms;         /* HIP-event time of the trace kernel(s)          */
+  double resolve_ms;       /* HIP-event time of the resolve kernel(s)        */
+  uint32_t trace_launches; /* number of trace launches (slabs)               */
+  uint32_t waves;          /* persistent waves per trace launch              */
+} RtRenderStats;
+
+/* spp 16, depth 8 (lib.rs:51), COUNTER, seed 2547549, one rank, device -1. */
+void rt_default_options(RtRenderOptions *opts);
+
+/* Rows of a `height`-row image that belong to `rank` (see RtRenderOptions). */
+size_t rt_tile_rows(size_t height, uint32_t row_block, uint32_t rank, uint32_t nranks);
+/* Image row (0 = top) of the k-th row of rank's tile. */
+size_t rt_tile_row(size_t k, uint32_t row_block, uint32_t rank, uint32_t nranks);
+
+/* Counter-mode seed of global sample `job` (splitmix64 finaliser, nonzero). */
+uint32_t rt_sample_seed(uint32_t seed, uint64_t job);
+
+/* Renders `framebuffer` (full image size) with explicit options.  pixels
+ * receives rank's tile: rt_tile_rows() rows of `width` pixels, tile row k =
+ * image row rt_tile_row(k).  Synchronous.  Returns 0 or a negative error. */
+int rt_render_ex(Rust_CFramebuffer framebuffer, const Rust_WorldHandle *handle,
+                 const RtRenderOptions *opts, RtRenderStats *stats);
+
+/* Same, but the tile is written to DEVICE memory `d_rgba` (rt_tile_rows*width
+ * RGBA8) on HIP stream `hip_stream` (NULL = the library's stream).  The scene
+ * stays resident on the device between calls.  Returns after the frame is
+ * complete.  Returns 0 or a negative error. */
+int rt_render_device(const Rust_WorldHandle *handle, size_t width, size_t height,
+                     const RtRenderOptions *opts, void *d_rgba, void *hip_stream,
+                     RtRenderStats *stats);
+
+/* Diagnostics: copies the per-sample colours (r, g, b, 0 as 4 f32) of the
+ * LAST trace launch on `device` (-1 = current) to host `out` (n floats max).
+ * Job order = tile pixel-major, sample-minor: job = (k*width + col)*spp + s
+ * for tile row k.  Returns the number of floats copied or a negative error. */
+long rt_read_samples(const Rust_WorldHandle *handle, int device, float *out, size_t n);
+
+/* Frees a handle from load_world (the reference never frees, lib.rs:42-45). */
+void rt_free_world(Rust_WorldHandle *handle);
+
+/* Last error message of this thread ("" if none). */
+const char *rt_last_error(void);
+
+/* Host-side scene introspection (no GPU needed). */
+size_t rt_world_num_spheres(const Rust_WorldHandle *handle);
+size_t rt_world_num_triangles(const Rust_WorldHandle *handle);
+/* center(3) radius material(type, r, g, b, a, param) */
+int rt_world_sphere(const Rust_WorldHandle *handle, size_t i, float out[10]);
+/* v0 v1 v2 normal material(type, r, g, b, a, param) */
+int rt_world_triangle(const Rust_WorldHandle *handle, size_t i, float out[18]);
+/* origin, lower_left_corner, horizontal, vertical (camera.rs:8-15) */
+void rt_camera_get(const Rust_Camera *camera, float out[12]);
+/* ParseError discriminant of the last failed load_world (parser.rs:11-18),
+ * 100 = input on which the reference panics, -1 = none. */
+int rt_last_parse_error(void);
+
+/* image.rs:59-81: writes an ASCII PPM (P3).  Returns 0 on success. */
+int rt_write_ppm(const Rust_CFramebuffer *framebuffer, const char *path);
+
+/* Number of HIP devices visible (0 if the runtime is unavailable). */
+int rt_device_count(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* RAYTRACER_AMD_H */

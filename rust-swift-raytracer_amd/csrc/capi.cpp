@@ -1,0 +1,202 @@
+// capi.cpp -- the C-ABI of the library: the reference's three entry points
+// (Naxaes/Rust-Swift-Raytracer raytracer/src/lib.rs:37-63, header
+// MacOSPlatform/MacOSPlatform/Engine/includes/raytracer.h:42-47) plus the
+// extensions declared in include/raytracer_amd.h.
+#include <cstdio>
+#include <cstring>
+#include <string>
+
+#include "../../include/raytracer.h"
+#include "../../include/raytracer_amd.h"
+#include "runtime.h"
+#include "scene.h"
+
+// The opaque types of raytracer.h.  Rust_WorldHandle stays two pointers;
+// the camera is heap-allocated on its own because callers replace it
+// (GameView.swift:200-216 writes handle->camera = move_camera_position(...)).
+struct Rust_World {
+    rtamd::WorldState state;
+};
+struct Rust_Camera {
+    rtamd::CameraModel cam;
+};
+
+namespace {
+thread_local int g_parse_status = rtamd::kParseOk;
+
+RtRenderOptions reference_options() {
+    RtRenderOptions o;
+    rt_default_options(&o);
+    return o;
+}
+}  // namespace
+
+extern "C" {
+
+// lib.rs:37-46
+Rust_WorldHandle *load_world(const char *source) {
+    if (!source) {
+        rtamd::set_error("load_world: null source");
+        return nullptr;
+    }
+    auto *world = new Rust_World();
+    g_parse_status = rtamd::parse_scene(std::string(source), world->state.scene);
+    if (g_parse_status != rtamd::kParseOk) {
+        rtamd::set_error("load_world: parse error " + std::to_string(g_parse_status));
+        delete world;
+        return nullptr;
+    }
+    // spheres padded to the kernel's scalar-load batch of 8 with NaN centres
+    world->state.packed = rtamd::pack_scene(world->state.scene, 8, 1);
+    auto *cam = new Rust_Camera{world->state.scene.camera};
+    return new Rust_WorldHandle{world, cam};
+}
+
+// lib.rs:60-63: consumes the old camera, returns Camera::new_at(pos + d, aspect).
+Rust_Camera *move_camera_position(Rust_Camera *camera, float x, float y, float z) {
+    if (!camera) return nullptr;
+    auto *moved = new Rust_Camera{rtamd::camera_moved(camera->cam, x, y, z)};
+    delete camera;
+    return moved;
+}
+
+// lib.rs:49-57: Options::new(16, 8, None, true); synchronous.  Writes into the
+// caller's pixels (the reference returned a pointer into a freed Vec).
+Rust_CFramebuffer render(Rust_CFramebuffer framebuffer, const Rust_WorldHandle *handle) {
+    RtRenderOptions o = reference_options();
+    int rc = rt_render_ex(framebuffer, handle, &o, nullptr);
+    if (rc != 0) {
+        std::fprintf(stderr, "raytracer render() failed (%d): %s\n", rc, rtamd::last_error().c_str());
+        return Rust_CFramebuffer{0, 0, nullptr};
+    }
+    return framebuffer;
+}
+
+void rt_default_options(RtRenderOptions *o) {
+    std::memset(o, 0, sizeof(*o));
+    o->samples_per_pixel = 16;  // lib.rs:51
+    o->max_ray_bounces = 8;     // lib.rs:51
+    o->rng_mode = RT_RNG_COUNTER;
+    o->seed = 2547549u;         // random.rs:9
+    o->row_block = 1;
+    o->rank = 0;
+    o->nranks = 1;
+    o->device = -1;
+}
+
+size_t rt_tile_rows(size_t height, uint32_t row_block, uint32_t rank, uint32_t nranks) {
+    if (rank >= (nranks ? nranks : 1)) return 0;
+    return rtamd::tile_rows(height, row_block, rank, nranks);
+}
+
+size_t rt_tile_row(size_t k, uint32_t row_block, uint32_t rank, uint32_t nranks) {
+    return rtamd::tile_row(k, row_block, rank, nranks);
+}
+
+uint32_t rt_sample_seed(uint32_t seed, uint64_t job) {
+    uint64_t z = job + (uint64_t)seed * 0x9E3779B97F4A7C15ull + 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    z ^= z >> 31;
+    uint32_t r = (uint32_t)(z ^ (z >> 32));
+    return r ? r : 2547549u;
+}
+
+int rt_render_ex(Rust_CFramebuffer fb, const Rust_WorldHandle *h, const RtRenderOptions *opts,
+                 RtRenderStats *stats) {
+    if (!h || !h->world || !h->camera) {
+        rtamd::set_error("render: null world handle");
+        return -1;
+    }
+    RtRenderOptions o = opts ? *opts : reference_options();
+    return rtamd::render_frame_host(h->world->state, h->camera->cam, fb.width, fb.height, o,
+                                    fb.pixels, stats);
+}
+
+int rt_render_device(const Rust_WorldHandle *h, size_t width, size_t height,
+                     const RtRenderOptions *opts, void *d_rgba, void *hip_stream,
+                     RtRenderStats *stats) {
+    if (!h || !h->world || !h->camera) {
+        rtamd::set_error("render: null world handle");
+        return -1;
+    }
+    RtRenderOptions o = opts ? *opts : reference_options();
+    return rtamd::render_frame(h->world->state, h->camera->cam, width, height, o,
+                               static_cast<uint32_t *>(d_rgba),
+                               static_cast<hipStream_t>(hip_stream), stats);
+}
+
+long rt_read_samples(const Rust_WorldHandle *h, int device, float *out, size_t n) {
+    if (!h || !h->world || !out) {
+        rtamd::set_error("rt_read_samples: null argument");
+        return -1;
+    }
+    return rtamd::read_samples(h->world->state, device, out, n);
+}
+
+void rt_free_world(Rust_WorldHandle *h) {
+    if (!h) return;
+    delete h->world;
+    delete h->camera;
+    delete h;
+}
+
+const char *rt_last_error(void) { return rtamd::last_error().c_str(); }
+
+int rt_last_parse_error(void) { return g_parse_status; }
+
+size_t rt_world_num_spheres(const Rust_WorldHandle *h) {
+    return h && h->world ? h->world->state.scene.spheres.size() : 0;
+}
+size_t rt_world_num_triangles(const Rust_WorldHandle *h) {
+    return h && h->world ? h->world->state.scene.triangles.size() : 0;
+}
+
+static void material_out(const rtamd::Material &m, float *o) {
+    o[0] = (float)m.kind; o[1] = m.r; o[2] = m.g; o[3] = m.b; o[4] = m.a; o[5] = m.param;
+}
+
+int rt_world_sphere(const Rust_WorldHandle *h, size_t i, float out[10]) {
+    if (!h || !h->world || i >= h->world->state.scene.spheres.size()) return -1;
+    const auto &sc = h->world->state.scene;
+    const auto &s = sc.spheres[i];
+    out[0] = s.center.x; out[1] = s.center.y; out[2] = s.center.z; out[3] = s.radius;
+    material_out(sc.materials[s.material], out + 4);
+    return 0;
+}
+
+int rt_world_triangle(const Rust_WorldHandle *h, size_t i, float out[18]) {
+    if (!h || !h->world || i >= h->world->state.scene.triangles.size()) return -1;
+    const auto &sc = h->world->state.scene;
+    const auto &t = sc.triangles[i];
+    const rtamd::Vec3 v[4] = {t.v0, t.v1, t.v2, t.normal};
+    for (int k = 0; k < 4; ++k) { out[3 * k] = v[k].x; out[3 * k + 1] = v[k].y; out[3 * k + 2] = v[k].z; }
+    material_out(sc.materials[t.material], out + 12);
+    return 0;
+}
+
+void rt_camera_get(const Rust_Camera *c, float out[12]) {
+    const rtamd::Vec3 v[4] = {c->cam.origin, c->cam.lower_left, c->cam.horizontal, c->cam.vertical};
+    for (int k = 0; k < 4; ++k) { out[3 * k] = v[k].x; out[3 * k + 1] = v[k].y; out[3 * k + 2] = v[k].z; }
+}
+
+// image.rs:59-81: "P3\n{w} {h}\n255\n" then "r g b\n" per pixel, top row first.
+int rt_write_ppm(const Rust_CFramebuffer *fb, const char *path) {
+    if (!fb || !path || (!fb->pixels && fb->width * fb->height)) return -1;
+    FILE *f = std::fopen(path, "wb");
+    if (!f) return -1;
+    std::fprintf(f, "P3\n%zu %zu\n255\n", fb->width, fb->height);
+    for (size_t i = 0; i < fb->width * fb->height; ++i) {
+        const Rust_ColorU8 &c = fb->pixels[i];
+        std::fprintf(f, "%u %u %u\n", (unsigned)c.r, (unsigned)c.g, (unsigned)c.b);
+    }
+    return std::fclose(f) == 0 ? 0 : -1;
+}
+
+int rt_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+}  // extern "C"

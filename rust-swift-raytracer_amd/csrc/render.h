@@ -1,0 +1,43 @@
+// render.h -- kernel launch interface of the HIP render path (internal).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace rtamd {
+
+enum : uint32_t { kRngCounter = 1, kRngReplay = 2 };
+enum : uint32_t { kMatDiffuse = 0, kMatMetal = 1, kMatDielectric = 2, kMatEmission = 3 };
+
+// Kernel argument block (lives in the kernarg segment -> SGPRs).
+struct TraceParams {
+    const float4 *sph_hot;    // nsph_padded x (cx, cy, cz, r*r); pad = NaN (never hit)
+    const float4 *sph_cold;   // nsph_padded x (r, material id bits, 0, 0)
+    const float4 *tri_hot;    // ntri x (n.x, n.y, n.z, n.v0), n = cross(v1-v0, v2-v0)
+    const float4 *tri_geo;    // ntri x 4: (v0, mat) (v1, 0) (v2, 0) (unit normal, 0)
+    const float *mats;        // 8 floats per material: kind bits, r, g, b, param
+    float4 *samples;          // slab-local per-sample colour (r, g, b, 0)
+    uint32_t *job_counter;    // zeroed before every launch
+    unsigned long long *stats;// [0] rays, [1] triangle tests in t-range
+    const uint32_t *replay;   // REPLAY start states (global job index)
+    float cam[12];            // origin, lower_left, horizontal, vertical
+    float wden, hden;         // (width-1) as f32, (height-1) as f32
+    uint32_t nsph, nsph_padded, ntri;
+    uint32_t width, height, spp;
+    int32_t depth;            // max_ray_bounces (may be <= 0: zero colour)
+    uint32_t mode, seed;
+    uint32_t row_block, rank, nranks;
+    uint32_t slab_row0;       // first tile row of this launch
+    uint32_t njobs;           // samples in this launch
+    uint32_t chunk;           // jobs fetched per atomic by one wave
+};
+
+hipError_t launch_trace(const TraceParams &p, uint32_t blocks, hipStream_t stream);
+// inv_spp = 1.0 / (spp as f32) computed from the signed spp (common.rs:345).
+hipError_t launch_resolve_ex(const float4 *samples, uint32_t *out, uint32_t npix, uint32_t spp,
+                             float inv_spp, uint32_t width, uint32_t slab_row0,
+                             hipStream_t stream);
+hipError_t trace_occupancy(int *blocks_per_cu);
+
+}  // namespace rtamd

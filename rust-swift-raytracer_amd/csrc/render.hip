@@ -1,0 +1,360 @@
+// render.hip -- the MI355X render path: a persistent path-regenerating trace
+// kernel and an ordered resolve kernel, hand-written for gfx950 (CDNA4).
+//
+// Replaces the reference's ray_trace pixel loop and everything under it
+// (Naxaes/Rust-Swift-Raytracer raytracer/src/common.rs:263-361 ray_color /
+// ray_trace, common.rs:59-258 Sphere/Triangle/Mesh/World::hit,
+// materials.rs:30-102 scatter, camera.rs:84-89 cast_ray, random.rs:15-30).
+//
+// Numerics: every operation is one IEEE binary32 op in the reference's order
+// (-ffp-contract=off, correctly rounded divide/sqrt), so a sample started
+// from the same xorshift32 state produces the same bits as the reference.
+//
+// Work decomposition: one job = one pixel sample.  Each wave is
+// persistent: its 64 lanes trace one bounce per loop iteration; a lane whose
+// path ends writes the sample colour to a per-sample slab in HBM and takes
+// the next job (ballot + mbcnt prefix, one atomic per 256 jobs per wave), so
+// lanes never idle behind the longest path of their wave.  Spheres are read
+// with wave-uniform scalar loads (SGPR operands, scalar cache), never per lane.
+// The resolve kernel sums each pixel's samples in sample order (the
+// reference's sequential add_with_alpha, common.rs:338-340), applies the
+// gamma/`as u8` epilogue (:344-356) and stores RGBA8 rows top-first (:351).
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "render.h"
+
+#pragma clang fp contract(off)
+
+namespace rtamd {
+namespace {
+
+// ------------------------------------------------------------ device maths
+struct F3 { float x, y, z; };
+
+__device__ __forceinline__ F3 f3(float x, float y, float z) { return F3{x, y, z}; }
+__device__ __forceinline__ F3 operator+(F3 a, F3 b) { return F3{a.x + b.x, a.y + b.y, a.z + b.z}; }
+__device__ __forceinline__ F3 operator-(F3 a, F3 b) { return F3{a.x - b.x, a.y - b.y, a.z - b.z}; }
+__device__ __forceinline__ F3 operator-(F3 a) { return F3{-a.x, -a.y, -a.z}; }
+__device__ __forceinline__ F3 scale(F3 a, float s) { return F3{a.x * s, a.y * s, a.z * s}; }
+__device__ __forceinline__ F3 divide(F3 a, float s) { return F3{a.x / s, a.y / s, a.z / s}; }
+// (x*x' + y*y') + z*z'  (maths.rs:82)
+__device__ __forceinline__ float dot(F3 a, F3 b) { return (a.x * b.x + a.y * b.y) + a.z * b.z; }
+__device__ __forceinline__ F3 cross(F3 a, F3 b) {  // maths.rs:88-94
+    return F3{a.y * b.z - a.z * b.y, -(a.x * b.z - a.z * b.x), a.x * b.y - a.y * b.x};
+}
+__device__ __forceinline__ F3 unit(F3 a) {  // NVec3::new, maths.rs:111-118
+    float len = __builtin_sqrtf((a.x * a.x + a.y * a.y) + a.z * a.z);
+    return F3{a.x / len, a.y / len, a.z / len};
+}
+
+// xorshift32 (random.rs:22-30) and `x as f32 / u32::MAX as f32` == x * 2^-32.
+__device__ __forceinline__ float draw01(uint32_t &s) {
+    uint32_t x = s;
+    x ^= x << 13;
+    x ^= x >> 17;
+    x ^= x << 5;
+    s = x;
+    return (float)x * 0x1p-32f;
+}
+__device__ __forceinline__ float draw11(uint32_t &s) { return draw01(s) * 2.0f - 1.0f; }
+// common.rs:32-38 -- three draws x, y, z, normalised (no rejection sampling).
+__device__ __forceinline__ F3 draw_unit(uint32_t &s) {
+    float x = draw11(s);
+    float y = draw11(s);
+    float z = draw11(s);
+    return unit(F3{x, y, z});
+}
+
+__device__ __forceinline__ uint32_t counter_seed(uint32_t seed, uint64_t job) {
+    uint64_t z = job + (uint64_t)seed * 0x9E3779B97F4A7C15ull + 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    z ^= z >> 31;
+    uint32_t r = (uint32_t)(z ^ (z >> 32));
+    return r ? r : 2547549u;
+}
+
+// Rust `f32 as u8`: saturating, NaN -> 0, truncating.
+__device__ __forceinline__ uint32_t sat_u8(float x) {
+    if (!(x > 0.0f)) return 0u;
+    if (x >= 255.0f) return 255u;
+    return (uint32_t)x;
+}
+
+// Wave-uniform read of scene data through the constant address space, so the
+// backend emits s_load (scalar cache -> SGPRs) instead of 64 lane loads.
+__device__ __forceinline__ float4 uniform_load(const float4 *base, uint32_t i) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    typedef const __attribute__((address_space(4))) float *cfloat_ptr;
+    const cfloat_ptr q = (cfloat_ptr)(const void *)base + 4u * i;
+    return make_float4(q[0], q[1], q[2], q[3]);
+#else
+    return base[i];
+#endif
+}
+
+constexpr uint32_t kWave = 64;
+constexpr uint32_t kBatch = 8;  // spheres per scalar-load batch (sphere count padded to it)
+
+// ------------------------------------------------------------ trace kernel
+__global__ __launch_bounds__(256) void trace_kernel(TraceParams p) {
+    const uint32_t lane = __lane_id();
+    const float tmin = 0.001f;                 // common.rs:242, 250
+
+    F3 org = f3(0, 0, 0), dir = f3(0, 0, 0);
+    float thr_r = 1.0f, thr_g = 1.0f, thr_b = 1.0f;  // ray_color's final_color
+    uint32_t rng = 0, job = 0, bounce = 0;
+    bool active = false;
+    uint32_t rays = 0, tri_in = 0;
+
+    uint32_t pool_next = 0, pool_end = 0;  // wave-uniform job pool
+    bool exhausted = false;
+
+    for (;;) {
+        // ---- refill lanes whose path ended (active-ray compaction) -------
+        const uint64_t dead = __ballot(!active);
+        if (dead != 0 && !exhausted) {
+            if (pool_next >= pool_end) {
+                uint32_t base = 0;
+                if (lane == 0) base = atomicAdd(p.job_counter, p.chunk);
+                base = __builtin_amdgcn_readfirstlane(base);
+                if (base >= p.njobs) {
+                    exhausted = true;
+                } else {
+                    pool_next = base;
+                    pool_end = min(base + p.chunk, p.njobs);
+                }
+            }
+            const uint32_t avail = pool_end - pool_next;
+            const uint32_t rank = __builtin_amdgcn_mbcnt_hi(
+                (uint32_t)(dead >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)dead, 0u));
+            if (!active && rank < avail) {
+                job = pool_next + rank;
+                // job -> (tile row, column, sample) -> reference (row, col)
+                const uint32_t lp = job / p.spp;
+                const uint32_t s = job - lp * p.spp;
+                const uint32_t q = lp / p.width;
+                const uint32_t col = lp - q * p.width;
+                const uint32_t lr = p.slab_row0 + q;
+                const uint32_t ir = ((lr / p.row_block) * p.nranks + p.rank) * p.row_block +
+                                    lr % p.row_block;
+                const uint32_t row = p.height - 1u - ir;
+                const uint64_t gjob = ((uint64_t)row * p.width + col) * p.spp + s;
+                rng = (p.mode == kRngReplay) ? p.replay[gjob] : counter_seed(p.seed, gjob);
+                // common.rs:335-337: u drawn before v; camera.rs:84-89
+                const float u = ((float)col + draw01(rng)) / p.wden;
+                const float v = ((float)row + draw01(rng)) / p.hden;
+                const F3 h = f3(p.cam[6], p.cam[7], p.cam[8]);
+                const F3 vv = f3(p.cam[9], p.cam[10], p.cam[11]);
+                org = f3(p.cam[0], p.cam[1], p.cam[2]);
+                const F3 llc = f3(p.cam[3], p.cam[4], p.cam[5]);
+                dir = unit(((llc + scale(h, u)) + scale(vv, v)) - org);
+                thr_r = thr_g = thr_b = 1.0f;
+                bounce = 0;
+                active = true;
+            }
+            pool_next += min((uint32_t)__popcll(dead), avail);
+        }
+        if (__ballot(active) == 0) {
+            if (exhausted) break;
+            continue;
+        }
+        if (!active) continue;
+
+        // ---- one iteration of ray_color's bounce loop (common.rs:267-282) --
+        bool done = false;
+        float out_r = 0.0f, out_g = 0.0f, out_b = 0.0f;
+        if ((int32_t)bounce >= p.depth) {
+            done = true;  // depth exhausted -> (0, 0, 0) (common.rs:284)
+        } else {
+            ++rays;
+            // World::hit, spheres in order with shrinking t_max (common.rs:241-247)
+            // Batches of kBatch spheres: all scalar loads issue up front, the
+            // discriminants (independent of t_max) are computed for the whole
+            // batch, and the in-order root/t_max updates run only when some
+            // lane's discriminant is non-negative (rare; wave-uniform skip).
+            float best_t = __builtin_inff();
+            int best_i = -1;
+            for (uint32_t i0 = 0; i0 < p.nsph_padded; i0 += kBatch) {
+                float hb[kBatch], disc[kBatch];
+                bool any = false;
+#pragma unroll
+                for (uint32_t k = 0; k < kBatch; ++k) {
+                    const float4 S = uniform_load(p.sph_hot, i0 + k);
+                    const float ocx = org.x - S.x, ocy = org.y - S.y, ocz = org.z - S.z;
+                    hb[k] = (ocx * dir.x + ocy * dir.y) + ocz * dir.z;
+                    const float cc = ((ocx * ocx + ocy * ocy) + ocz * ocz) - S.w;
+                    disc[k] = hb[k] * hb[k] - cc;  // a == 1.0 exactly (maths.rs:127)
+                    any |= disc[k] >= 0.0f;
+                }
+                if (!any) continue;
+#pragma unroll
+                for (uint32_t k = 0; k < kBatch; ++k) {
+                    if (disc[k] >= 0.0f) {
+                        const float sq = __builtin_sqrtf(disc[k]);
+                        const float r1 = -hb[k] - sq;
+                        const float r2 = -hb[k] + sq;
+                        const bool ok1 = (tmin < r1) && (r1 < best_t);
+                        const bool ok2 = (tmin < r2) && (r2 < best_t);
+                        if (ok1 || ok2) {
+                            best_t = ok1 ? r1 : r2;  // r1 <= r2: the smaller valid root
+                            best_i = (int)(i0 + k);
+                        }
+                    }
+                }
+            }
+            // Mesh::hit with t_max = best_t, own closest from +inf (common.rs:178-223)
+            float tri_t = __builtin_inff();
+            int tri_i = -1;
+            for (uint32_t j = 0; j < p.ntri; ++j) {
+                const float4 N = p.tri_hot[j];
+                const float cosl = (N.x * dir.x + N.y * dir.y) + N.z * dir.z;
+                if (-1e-8f < cosl && cosl < 1e-8f) continue;
+                const float t = (((N.x * org.x + N.y * org.y) + N.z * org.z) + N.w) / cosl;
+                if (t < tmin || t > best_t) continue;
+                ++tri_in;
+                const F3 n = f3(N.x, N.y, N.z);
+                const F3 pt = org + scale(dir, t);
+                const float4 *g = p.tri_geo + 4u * j;
+                const float4 A = g[0], B = g[1], Cc = g[2];
+                const F3 v0 = f3(A.x, A.y, A.z), v1 = f3(B.x, B.y, B.z), v2 = f3(Cc.x, Cc.y, Cc.z);
+                if (dot(n, cross(v1 - v0, pt - v0)) < 0.0f) continue;
+                if (dot(n, cross(v2 - v1, pt - v1)) < 0.0f) continue;
+                if (dot(n, cross(v0 - v2, pt - v2)) < 0.0f) continue;
+                if (t < tri_t) { tri_t = t; tri_i = (int)j; }
+            }
+
+            if (tri_i < 0 && best_i < 0) {
+                // background (common.rs:276-281): re-normalise, lerp to sky blue
+                const float t = 0.5f * (unit(dir).y + 1.0f);
+                const float w = 1.0f - t;
+                out_r = thr_r * (1.0f * w + 0.5f * t);
+                out_g = thr_g * (1.0f * w + 0.7f * t);
+                out_b = thr_b * (1.0f * w + 1.0f * t);
+                done = true;
+            } else {
+                F3 pos, nrm;
+                uint32_t mid;
+                if (tri_i >= 0) {  // a triangle wins a tie against a sphere
+                    pos = org + scale(dir, tri_t);
+                    const float4 *g = p.tri_geo + 4u * (uint32_t)tri_i;
+                    const float4 A = g[0], Nn = g[3];
+                    nrm = f3(Nn.x, Nn.y, Nn.z);
+                    mid = __float_as_uint(A.w);
+                } else {
+                    const float4 S = p.sph_hot[best_i];
+                    const float4 Sc = p.sph_cold[best_i];
+                    pos = org + scale(dir, best_t);
+                    nrm = unit(divide(pos - f3(S.x, S.y, S.z), Sc.x));  // common.rs:95
+                    mid = __float_as_uint(Sc.y);
+                }
+                const float *m = p.mats + 8u * mid;
+                const uint32_t kind = __float_as_uint(m[0]);
+                float cr = m[1], cg = m[2], cb = m[3];
+                bool next = true;
+                F3 ndir;
+                if (kind == kMatDiffuse) {  // materials.rs:42-52
+                    const F3 sc = nrm + draw_unit(rng);
+                    const float e = 1e-8f;
+                    const bool nz = fabsf(sc.x) < e && fabsf(sc.y) < e && fabsf(sc.z) < e;
+                    ndir = nz ? nrm : unit(sc);
+                } else if (kind == kMatMetal) {  // materials.rs:54-63
+                    const F3 refl = dir - scale(nrm, 2.0f * dot(dir, nrm));
+                    const F3 d2 = refl + scale(draw_unit(rng), m[4]);
+                    next = dot(d2, nrm) >= 0.0f;
+                    ndir = unit(d2);
+                } else if (kind == kMatDielectric) {  // materials.rs:65-97
+                    F3 n2 = nrm;
+                    float eta = m[4];
+                    if (dot(dir, nrm) >= 0.0f) { n2 = -nrm; eta = 1.0f / m[4]; }
+                    const float cos_t = dot(-dir, n2);  // maths.rs:31-36
+                    const F3 perp = scale(dir + scale(n2, cos_t), eta);
+                    const F3 par = scale(n2, -__builtin_sqrtf(fabsf(1.0f - dot(perp, perp))));
+                    ndir = unit(perp + par);
+                    cr = cg = cb = 1.0f;
+                } else {  // Emission (materials.rs:100-102)
+                    next = false;
+                }
+                if (next) {
+                    thr_r = thr_r * cr;
+                    thr_g = thr_g * cg;
+                    thr_b = thr_b * cb;
+                    org = pos;
+                    dir = ndir;
+                    ++bounce;
+                } else {  // common.rs:273-274: final * colour
+                    out_r = thr_r * cr;
+                    out_g = thr_g * cg;
+                    out_b = thr_b * cb;
+                    done = true;
+                }
+            }
+        }
+        if (done) {
+            p.samples[job] = make_float4(out_r, out_g, out_b, 0.0f);
+            active = false;
+        }
+    }
+
+    // ---- per-wave statistics: one atomic per counter per wave ------------
+    uint64_t r = rays, ti = tri_in;
+    for (uint32_t off = kWave / 2; off > 0; off >>= 1) {
+        r += __shfl_xor(r, (int)off);
+        ti += __shfl_xor(ti, (int)off);
+    }
+    if (lane == 0) {
+        atomicAdd(&p.stats[0], (unsigned long long)r);
+        atomicAdd(&p.stats[1], (unsigned long long)ti);
+    }
+}
+
+// ------------------------------------------------------------ resolve kernel
+// Sums each pixel's samples in order (common.rs:333-341), gamma + `as u8`
+// (:344-356), one RGBA8 word per pixel, coalesced along the row.
+__global__ __launch_bounds__(256) void resolve_kernel(const float4 *__restrict__ samples,
+                                                      uint32_t *__restrict__ out, uint32_t npix,
+                                                      uint32_t spp, float inv, uint32_t width,
+                                                      uint32_t slab_row0) {
+    const uint32_t lp = blockIdx.x * blockDim.x + threadIdx.x;
+    if (lp >= npix) return;
+    float r = 0.0f, g = 0.0f, b = 0.0f, a = 1.0f;  // Color::new(0,0,0): alpha 1
+    const float4 *s = samples + (size_t)lp * spp;
+    for (uint32_t k = 0; k < spp; ++k) {
+        const float4 c = s[k];
+        r = r + c.x;
+        g = g + c.y;
+        b = b + c.z;
+        a = a + 1.0f;  // every sample's alpha is exactly 1.0
+    }
+    const uint32_t R = sat_u8(__builtin_sqrtf(r * inv) * 255.999f);
+    const uint32_t G = sat_u8(__builtin_sqrtf(g * inv) * 255.999f);
+    const uint32_t B = sat_u8(__builtin_sqrtf(b * inv) * 255.999f);
+    const uint32_t A = sat_u8(a * inv * 255.999f);
+    const uint32_t q = lp / width;
+    const uint32_t col = lp - q * width;
+    out[(size_t)(slab_row0 + q) * width + col] = R | (G << 8) | (B << 16) | (A << 24);
+}
+
+}  // namespace
+
+hipError_t launch_trace(const TraceParams &p, uint32_t blocks, hipStream_t stream) {
+    hipLaunchKernelGGL(trace_kernel, dim3(blocks), dim3(256), 0, stream, p);
+    return hipGetLastError();
+}
+
+hipError_t launch_resolve_ex(const float4 *samples, uint32_t *out, uint32_t npix, uint32_t spp,
+                             float inv_spp, uint32_t width, uint32_t slab_row0,
+                             hipStream_t stream) {
+    const uint32_t blocks = (npix + 255u) / 256u;
+    hipLaunchKernelGGL(resolve_kernel, dim3(blocks), dim3(256), 0, stream, samples, out, npix,
+                       spp, inv_spp, width, slab_row0);
+    return hipGetLastError();
+}
+
+hipError_t trace_occupancy(int *blocks_per_cu) {
+    return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, trace_kernel, 256, 0);
+}
+
+}  // namespace rtamd

@@ -1,0 +1,267 @@
+// runtime.cpp -- frame driver of the HIP render path (host side).
+//
+// Owns each world's device-resident scene (uploaded once per device, reused
+// by every frame and every camera move), the per-sample slab and the launch
+// sequence: for every slab of tile rows, zero the job counter, launch the
+// persistent trace kernel, then the ordered resolve kernel.  The reference's
+// equivalent is ray_trace's triple loop (common.rs:320-361).
+#include "runtime.h"
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+
+#include "../../include/raytracer_amd.h"
+#include "render.h"
+
+namespace rtamd {
+
+namespace {
+thread_local std::string g_error;
+
+uint64_t env_u64(const char *name, uint64_t dflt) {
+    const char *v = std::getenv(name);
+    if (!v || !*v) return dflt;
+    return std::strtoull(v, nullptr, 10);
+}
+}  // namespace
+
+void set_error(const std::string &msg) { g_error = msg; }
+const std::string &last_error() { return g_error; }
+
+#define HIP_TRY(expr)                                                                 \
+    do {                                                                              \
+        hipError_t e_ = (expr);                                                       \
+        if (e_ != hipSuccess) {                                                       \
+            set_error(std::string(#expr) + " failed: " + hipGetErrorString(e_));      \
+            return -2;                                                                \
+        }                                                                             \
+    } while (0)
+
+DeviceState::~DeviceState() {
+    if (device < 0) return;
+    if (hipSetDevice(device) != hipSuccess) return;
+    void *bufs[] = {sph_hot, sph_cold, tri_hot, tri_geo, mats, samples, out, replay, counter, stats};
+    for (void *b : bufs)
+        if (b) (void)hipFree(b);
+    for (hipEvent_t e : ev)
+        if (e) (void)hipEventDestroy(e);
+    if (stream) (void)hipStreamDestroy(stream);
+}
+
+size_t tile_rows(size_t height, uint32_t row_block, uint32_t rank, uint32_t nranks) {
+    if (nranks <= 1) return height;
+    const size_t B = row_block ? row_block : 1;
+    const size_t blocks = (height + B - 1) / B;
+    size_t rows = 0;
+    for (size_t b = rank; b < blocks; b += nranks) rows += std::min(B, height - b * B);
+    return rows;
+}
+
+size_t tile_row(size_t k, uint32_t row_block, uint32_t rank, uint32_t nranks) {
+    if (nranks <= 1) return k;
+    const size_t B = row_block ? row_block : 1;
+    return ((k / B) * nranks + rank) * B + k % B;
+}
+
+static int device_for(WorldState &w, int want, DeviceState *&out) {
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) {
+        set_error("no HIP device available: the MI355X render path requires a GPU");
+        return -3;
+    }
+    int dev = want;
+    if (dev < 0) HIP_TRY(hipGetDevice(&dev));
+    if (dev >= count) {
+        set_error("device ordinal out of range");
+        return -1;
+    }
+    HIP_TRY(hipSetDevice(dev));
+    auto &slot = w.devices[dev];
+    if (!slot) {
+        auto d = std::make_unique<DeviceState>();
+        d->device = dev;
+        HIP_TRY(hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking));
+        for (auto &e : d->ev) HIP_TRY(hipEventCreate(&e));
+        hipDeviceProp_t prop;
+        HIP_TRY(hipGetDeviceProperties(&prop, dev));
+        d->num_cus = prop.multiProcessorCount;
+        HIP_TRY(trace_occupancy(&d->blocks_per_cu));
+        const uint64_t bpc = env_u64("RT_AMD_BLOCKS_PER_CU", 0);
+        if (bpc) d->blocks_per_cu = (int)bpc;
+        if (d->blocks_per_cu < 1) d->blocks_per_cu = 1;
+        // scene upload (once per device)
+        const PackedScene &p = w.packed;
+        auto up = [&](void **dst, const std::vector<float> &src) -> hipError_t {
+            hipError_t e = hipMalloc(dst, src.size() * sizeof(float));
+            if (e != hipSuccess) return e;
+            return hipMemcpy(*dst, src.data(), src.size() * sizeof(float), hipMemcpyHostToDevice);
+        };
+        HIP_TRY(up((void **)&d->sph_hot, p.sph_hot));
+        HIP_TRY(up((void **)&d->sph_cold, p.sph_cold));
+        HIP_TRY(up((void **)&d->tri_hot, p.tri_hot));
+        HIP_TRY(up((void **)&d->tri_geo, p.tri_geo));
+        HIP_TRY(up((void **)&d->mats, p.mats));
+        d->nsph = p.nsph;
+        d->nsph_padded = p.nsph_padded;
+        d->ntri = p.ntri;
+        HIP_TRY(hipMalloc((void **)&d->counter, 64));
+        HIP_TRY(hipMalloc((void **)&d->stats, 64));
+        slot = std::move(d);
+    }
+    out = slot.get();
+    return 0;
+}
+
+template <typename T>
+static hipError_t grow(T *&buf, size_t &cap, size_t n) {
+    if (n <= cap) return hipSuccess;
+    if (buf) (void)hipFree(buf);
+    buf = nullptr;
+    cap = 0;
+    hipError_t e = hipMalloc((void **)&buf, n * sizeof(T));
+    if (e == hipSuccess) cap = n;
+    return e;
+}
+
+int render_frame(WorldState &w, const CameraModel &cam, size_t width, size_t height,
+                 const RtRenderOptions &o, uint32_t *d_out, hipStream_t stream,
+                 RtRenderStats *stats) {
+    if (stats) std::memset(stats, 0, sizeof(*stats));
+    const uint32_t nranks = o.nranks ? o.nranks : 1;
+    if (o.rank >= nranks) { set_error("rank >= nranks"); return -1; }
+    if (o.rng_mode != RT_RNG_COUNTER && o.rng_mode != RT_RNG_REPLAY) {
+        set_error("rng_mode must be RT_RNG_COUNTER or RT_RNG_REPLAY");
+        return -1;
+    }
+    if (o.rng_mode == RT_RNG_REPLAY && !o.replay_states) { set_error("replay table missing"); return -1; }
+    if (width > 0xFFFFFFu || height > 0xFFFFFFu) { set_error("frame too large"); return -1; }
+    const uint32_t B = nranks > 1 ? (o.row_block ? o.row_block : 1) : (uint32_t)std::max<size_t>(height, 1);
+    const size_t T = tile_rows(height, B, o.rank, nranks);
+    if (width == 0 || T == 0) return 0;
+    if (!d_out) { set_error("null output"); return -1; }
+
+    DeviceState *d = nullptr;
+    int rc = device_for(w, o.device, d);
+    if (rc) return rc;
+    hipStream_t s = stream ? stream : d->stream;
+
+    const uint32_t spp = o.samples_per_pixel > 0 ? (uint32_t)o.samples_per_pixel : 0u;
+    const uint64_t jobs_per_row = (uint64_t)width * spp;
+    if (jobs_per_row > 0x7FFFFFFFull) { set_error("width*spp too large"); return -1; }
+    const uint64_t slab_jobs = env_u64("RT_AMD_SLAB_JOBS", 1ull << 28);
+    size_t rows_per_slab = jobs_per_row ? (size_t)std::max<uint64_t>(1, slab_jobs / jobs_per_row) : T;
+    rows_per_slab = std::min(rows_per_slab, T);
+    if (jobs_per_row) HIP_TRY(grow(d->samples, d->samples_cap, rows_per_slab * jobs_per_row));
+
+    if (o.rng_mode == RT_RNG_REPLAY && spp) {
+        const size_t n = width * height * (size_t)spp;
+        HIP_TRY(grow(d->replay, d->replay_cap, n));
+        HIP_TRY(hipMemcpyAsync(d->replay, o.replay_states, n * 4, hipMemcpyHostToDevice, s));
+    }
+    HIP_TRY(hipMemsetAsync(d->stats, 0, 16, s));
+
+    TraceParams p{};
+    p.sph_hot = d->sph_hot; p.sph_cold = d->sph_cold;
+    p.tri_hot = d->tri_hot; p.tri_geo = d->tri_geo;
+    p.mats = d->mats;
+    p.samples = d->samples;
+    p.job_counter = d->counter;
+    p.stats = d->stats;
+    p.replay = d->replay;
+    const Vec3 cv[4] = {cam.origin, cam.lower_left, cam.horizontal, cam.vertical};
+    for (int i = 0; i < 4; ++i) { p.cam[3 * i] = cv[i].x; p.cam[3 * i + 1] = cv[i].y; p.cam[3 * i + 2] = cv[i].z; }
+    p.wden = (float)(uint64_t)(width - 1);   // (width-1) as f32 (common.rs:335)
+    p.hden = (float)(uint64_t)(height - 1);  // (height-1) as f32 (common.rs:336)
+    p.nsph = d->nsph; p.nsph_padded = d->nsph_padded; p.ntri = d->ntri;
+    p.width = (uint32_t)width; p.height = (uint32_t)height; p.spp = spp;
+    p.depth = o.max_ray_bounces;
+    p.mode = o.rng_mode; p.seed = o.seed;
+    p.row_block = B; p.rank = o.rank; p.nranks = nranks;
+    const float inv_spp = 1.0f / (float)o.samples_per_pixel;  // 1.0 / spp as f32 (common.rs:345)
+
+    const uint64_t full_blocks = (uint64_t)d->blocks_per_cu * (uint64_t)d->num_cus;
+    double trace_ms = 0.0, resolve_ms = 0.0;
+    uint32_t launches = 0, waves = 0;
+    for (size_t r0 = 0; r0 < T; r0 += rows_per_slab) {
+        const size_t rows = std::min(rows_per_slab, T - r0);
+        const uint64_t njobs = rows * jobs_per_row;
+        p.slab_row0 = (uint32_t)r0;
+        p.njobs = (uint32_t)njobs;
+        HIP_TRY(hipEventRecord(d->ev[0], s));
+        if (njobs) {
+            uint64_t blocks = std::min<uint64_t>(full_blocks, (njobs + 1023) / 1024);
+            blocks = std::max<uint64_t>(blocks, 1);
+            const uint64_t nwaves = blocks * 4;
+            uint64_t chunk = env_u64("RT_AMD_CHUNK", 0);
+            if (!chunk) chunk = std::min<uint64_t>(256, std::max<uint64_t>(64, njobs / (nwaves * 16) / 64 * 64));
+            p.chunk = (uint32_t)chunk;
+            HIP_TRY(hipMemsetAsync(d->counter, 0, 4, s));
+            HIP_TRY(launch_trace(p, (uint32_t)blocks, s));
+            d->last_jobs = njobs;
+            ++launches;
+            waves = (uint32_t)nwaves;
+        }
+        HIP_TRY(hipEventRecord(d->ev[1], s));
+        HIP_TRY(launch_resolve_ex(d->samples, d_out, (uint32_t)(rows * width), spp, inv_spp,
+                                  (uint32_t)width, (uint32_t)r0, s));
+        HIP_TRY(hipEventRecord(d->ev[2], s));
+        HIP_TRY(hipEventSynchronize(d->ev[2]));
+        float a = 0, b = 0;
+        HIP_TRY(hipEventElapsedTime(&a, d->ev[0], d->ev[1]));
+        HIP_TRY(hipEventElapsedTime(&b, d->ev[1], d->ev[2]));
+        trace_ms += a;
+        resolve_ms += b;
+    }
+    unsigned long long st[2] = {0, 0};
+    HIP_TRY(hipMemcpyAsync(st, d->stats, 16, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    if (stats) {
+        stats->samples = (uint64_t)T * jobs_per_row;
+        stats->rays = st[0];
+        stats->sphere_tests = st[0] * (uint64_t)d->nsph;
+        stats->tri_tests = st[0] * (uint64_t)d->ntri;
+        stats->tri_in_range = st[1];
+        stats->trace_ms = trace_ms;
+        stats->resolve_ms = resolve_ms;
+        stats->trace_launches = launches;
+        stats->waves = waves;
+    }
+    return 0;
+}
+
+long read_samples(WorldState &w, int device, float *out, size_t n) {
+    DeviceState *d = nullptr;
+    int rc = device_for(w, device, d);
+    if (rc) return rc;
+    const size_t count = std::min(n / 4, d->last_jobs);
+    if (!count) return 0;
+    HIP_TRY(hipStreamSynchronize(d->stream));
+    HIP_TRY(hipMemcpy(out, d->samples, count * sizeof(float4), hipMemcpyDeviceToHost));
+    return (long)(count * 4);
+}
+
+int render_frame_host(WorldState &w, const CameraModel &cam, size_t width, size_t height,
+                      const RtRenderOptions &o, void *host_out, RtRenderStats *stats) {
+    const uint32_t nranks = o.nranks ? o.nranks : 1;
+    const uint32_t B = nranks > 1 ? (o.row_block ? o.row_block : 1) : (uint32_t)std::max<size_t>(height, 1);
+    const size_t T = o.rank < nranks ? tile_rows(height, B, o.rank, nranks) : 0;
+    if (width == 0 || T == 0) {
+        if (stats) std::memset(stats, 0, sizeof(*stats));
+        return o.rank < nranks ? 0 : -1;
+    }
+    if (!host_out) { set_error("null framebuffer pixels"); return -1; }
+    DeviceState *d = nullptr;
+    int rc = device_for(w, o.device, d);
+    if (rc) return rc;
+    HIP_TRY(grow(d->out, d->out_cap, T * width));
+    rc = render_frame(w, cam, width, height, o, d->out, d->stream, stats);
+    if (rc) return rc;
+    HIP_TRY(hipMemcpyAsync(host_out, d->out, T * width * 4, hipMemcpyDeviceToHost, d->stream));
+    HIP_TRY(hipStreamSynchronize(d->stream));
+    return 0;
+}
+
+}  // namespace rtamd

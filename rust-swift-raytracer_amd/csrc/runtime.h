@@ -1,0 +1,62 @@
+// runtime.h -- device-side state of a loaded world and the frame driver.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <map>
+#include <memory>
+#include <string>
+
+#include "scene.h"
+
+struct RtRenderOptions;
+struct RtRenderStats;
+
+namespace rtamd {
+
+void set_error(const std::string &msg);
+const std::string &last_error();
+
+// One device's copy of a scene plus the scratch a frame needs.  Buffers grow
+// on demand and persist across frames (the interactive flow re-renders the
+// same scene with a moved camera, GameView.swift:198-219 / lib.rs:60-63).
+struct DeviceState {
+    int device = -1;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
+    float4 *sph_hot = nullptr, *sph_cold = nullptr, *tri_hot = nullptr, *tri_geo = nullptr;
+    float *mats = nullptr;
+    uint32_t nsph = 0, nsph_padded = 0, ntri = 0;
+    float4 *samples = nullptr;       size_t samples_cap = 0;   // per-sample colour slab
+    uint32_t *out = nullptr;         size_t out_cap = 0;       // RGBA8 tile (host path)
+    uint32_t *replay = nullptr;      size_t replay_cap = 0;
+    uint32_t *counter = nullptr;                                // job counter
+    unsigned long long *stats = nullptr;                        // [rays, tri_in_range]
+    int blocks_per_cu = 0, num_cus = 0;
+    size_t last_jobs = 0;                                       // jobs of the last launch
+    ~DeviceState();
+};
+
+struct WorldState {
+    SceneModel scene;
+    PackedScene packed;
+    std::map<int, std::unique_ptr<DeviceState>> devices;
+};
+
+// Renders rank's tile of a width x height frame into device memory d_out
+// (RGBA8 words, tile row-major).  stream may be null (library stream).
+int render_frame(WorldState &w, const CameraModel &cam, size_t width, size_t height,
+                 const RtRenderOptions &opts, uint32_t *d_out, hipStream_t stream,
+                 RtRenderStats *stats);
+
+// Same, into host memory (the reference's synchronous render(), lib.rs:49-57).
+int render_frame_host(WorldState &w, const CameraModel &cam, size_t width, size_t height,
+                      const RtRenderOptions &opts, void *host_out, RtRenderStats *stats);
+
+long read_samples(WorldState &w, int device, float *out, size_t n);
+
+size_t tile_rows(size_t height, uint32_t row_block, uint32_t rank, uint32_t nranks);
+size_t tile_row(size_t k, uint32_t row_block, uint32_t rank, uint32_t nranks);
+
+}  // namespace rtamd

@@ -1,0 +1,222 @@
+"""GPU parity: the HIP render path (through the C-ABI) against the CPU oracle.
+
+Bar: bit-exact.  Every comparison below is on raw bits -- the RGBA8 frame
+and, where the frame fits one launch, every sample's float colour.
+  * REPLAY mode vs the oracle's SERIAL mode (the reference's semantics, one
+    frame-wide xorshift32 stream, common.rs:321): the GPU reproduces the
+    reference render bit-for-bit when given each sample's start state.
+  * COUNTER mode vs the oracle's COUNTER mode: bit-exact.
+  * COUNTER vs SERIAL: different RNG streams by construction -- statistical
+    bound only (mean |diff| and PSNR, thresholds in the test).
+At BASELINE sizes (1920x1080x64) the tests use size-independent properties:
+determinism, tile invariance and oracle parity on sampled rows.
+"""
+import numpy as np
+import pytest
+
+import oracle as O
+import raytracer_amd as R
+import scenes as S
+from conftest import scene_text
+
+pytestmark = pytest.mark.gpu
+
+CWORLD = "c_raytracer_world.txt"
+
+
+def oracle_samples_to_gpu_order(samples, width, height, spp):
+    """Oracle job = (row*W + col)*spp + s (row 0 = bottom); GPU tile order is
+    image row (top first) major."""
+    a = samples.reshape(height, width, spp, 4)[::-1]
+    return np.ascontiguousarray(a).reshape(-1, 4)
+
+
+def assert_bits_equal(a, b, what):
+    a = np.ascontiguousarray(a)
+    b = np.ascontiguousarray(b)
+    assert a.shape == b.shape, what
+    if a.dtype == np.float32:
+        a, b = a.view(np.uint32), b.view(np.uint32)
+    bad = np.argwhere(a != b)
+    assert bad.size == 0, f"{what}: {len(bad)} mismatches, first at {bad[:5].tolist()}"
+
+
+@pytest.mark.parametrize("scene,w,h,spp,depth", [
+    (CWORLD, 40, 30, 4, 8),
+    ("world.txt", 33, 17, 3, 8),
+    ("three_spheres.txt", 64, 64, 1, 4),
+])
+def test_replay_matches_reference_serial(scene, w, h, spp, depth):
+    src = scene_text(scene)
+    ref = O.Scene(src)
+    img, st, states, smp = ref.render(w, h, spp, depth, mode=O.RNG_SERIAL, record_states=True,
+                                      record_samples=True)
+    world = R.World(src)
+    out, gst = world.render(w, h, spp, depth, mode=R.RNG_REPLAY, replay=states)
+    assert_bits_equal(out, img, "frame")
+    assert_bits_equal(world.read_samples(w * h * spp)[:, :3],
+                      oracle_samples_to_gpu_order(smp, w, h, spp)[:, :3], "samples")
+    assert gst["rays"] == st["rays"]
+    assert gst["tri_in_range"] == st["tri_in_range"]
+    assert gst["sphere_tests"] == st["sphere_tests"]
+    assert gst["tri_tests"] == st["tri_tests"]
+
+
+def test_c1_three_spheres_full_frame_serial():
+    """BASELINE configs[0]: 256x256, 1 spp, depth 4, reference serial RNG."""
+    src = S.three_spheres()
+    img, st, states = O.Scene(src).render(256, 256, 1, 4, record_states=True)
+    out, gst = R.World(src).render(256, 256, 1, 4, mode=R.RNG_REPLAY, replay=states)
+    assert_bits_equal(out, img, "C1 frame")
+    assert gst["rays"] == st["rays"]
+
+
+def test_c_raytracer_example_frame_serial():
+    """examples/c_raytracer.rs: 200x200 via render() settings (16 spp, depth 8)."""
+    src = scene_text(CWORLD)
+    img, st, states = O.Scene(src).render(200, 200, 16, 8, record_states=True)
+    out, gst = R.World(src).render(200, 200, 16, 8, mode=R.RNG_REPLAY, replay=states)
+    assert_bits_equal(out, img, "c_raytracer frame")
+    assert gst["rays"] == st["rays"] and gst["tri_in_range"] == st["tri_in_range"]
+
+
+@pytest.mark.parametrize("scene,w,h,spp,depth,seed", [
+    (CWORLD, 48, 27, 8, 8, 2547549),
+    ("world.txt", 31, 23, 5, 6, 7),
+    ("rtow.txt", 64, 36, 4, 8, 2547549),
+])
+def test_counter_mode_bit_exact(scene, w, h, spp, depth, seed):
+    src = scene_text(scene)
+    img, st, _, smp = O.Scene(src).render(w, h, spp, depth, mode=O.RNG_COUNTER, seed=seed,
+                                          nthreads=8, record_samples=True)
+    world = R.World(src)
+    out, gst = world.render(w, h, spp, depth, mode=R.RNG_COUNTER, seed=seed)
+    assert_bits_equal(out, img, "frame")
+    assert_bits_equal(world.read_samples(w * h * spp)[:, :3],
+                      oracle_samples_to_gpu_order(smp, w, h, spp)[:, :3], "samples")
+    assert gst["rays"] == st["rays"]
+
+
+def test_render_abi_defaults_match_oracle_counter():
+    """render() (lib.rs:49-57 -> 16 spp, depth 8) == oracle COUNTER at 16/8."""
+    src = scene_text(CWORLD)
+    img, _, _ = O.Scene(src).render(96, 54, 16, 8, mode=O.RNG_COUNTER, nthreads=8)
+    out = R.World(src).render_reference(96, 54)
+    assert_bits_equal(out, img, "render()")
+
+
+def test_counter_vs_serial_statistics():
+    """Different RNG streams: compare converged images statistically."""
+    src = scene_text(CWORLD)
+    w, h, spp = 64, 64, 64
+    serial, _, _ = O.Scene(src).render(w, h, spp, 8, mode=O.RNG_SERIAL)
+    out, _ = R.World(src).render(w, h, spp, 8, mode=R.RNG_COUNTER)
+    d = np.abs(out[..., :3].astype(np.float64) - serial[..., :3].astype(np.float64))
+    mse = float((d ** 2).mean())
+    psnr = 10 * np.log10(255.0 ** 2 / mse)
+    assert d.mean() < 4.0, d.mean()          # mean |diff| under 4/255 at 64 spp
+    assert psnr > 28.0, psnr                 # Monte-Carlo noise only
+    assert (out[..., 3] == serial[..., 3]).all()
+
+
+@pytest.mark.parametrize("w,h,spp,depth", [
+    (1, 5, 2, 8),    # (width-1) == 0: u = inf -> NaN ray -> black pixel
+    (5, 1, 2, 8),
+    (6, 4, 0, 8),    # spp = 0: sqrt(0 * inf) = NaN -> 0, alpha 255
+    (6, 4, -2, 8),   # negative spp: no samples, negative reciprocal
+    (6, 4, 3, 0),    # depth 0: every sample is (0, 0, 0)
+    (6, 4, 3, -1),
+    (7, 3, 65, 3),   # spp > 64
+])
+def test_edge_cases(w, h, spp, depth):
+    src = scene_text(CWORLD)
+    img, st, states = O.Scene(src).render(w, h, spp, depth, record_states=True)
+    out, gst = R.World(src).render(w, h, spp, depth, mode=R.RNG_REPLAY,
+                                   replay=states if states.size else np.zeros(1, np.uint32))
+    assert_bits_equal(out, img, "edge frame")
+    assert gst["rays"] == st["rays"]
+
+
+def test_empty_and_triangle_only_scenes():
+    for src in ["camera origin 0.0 0.0 0.0 aspect 1.5;",
+                "camera origin 0.0 0.5 0.0 aspect 1.0;\nmaterial M : Metal color 0.9 0.2 0.2 fuzz 0.1;\n"
+                "triangle v0 -1.0 -1.0 -2.0 v1 1.0 -1.0 -2.0 v2 0.0 1.0 -2.5 material M;\n"
+                "triangle v0 -3.0 -0.5 -5.0 v1 3.0 -0.5 -5.0 v2 0.0 -0.5 3.0 material M;\n"]:
+        img, st, states = O.Scene(src).render(24, 16, 4, 8, record_states=True)
+        out, gst = R.World(src).render(24, 16, 4, 8, mode=R.RNG_REPLAY, replay=states)
+        assert_bits_equal(out, img, "frame")
+        assert gst["rays"] == st["rays"] and gst["tri_in_range"] == st["tri_in_range"]
+
+
+def test_mesh_scene_triangle_path():
+    """C5 scene (100k triangles + 100 spheres) at a size the oracle finishes."""
+    src = S.mesh()
+    w, h, spp = 16, 9, 1
+    img, st, _, smp = O.Scene(src).render(w, h, spp, 8, mode=O.RNG_COUNTER, nthreads=8,
+                                          record_samples=True)
+    world = R.World(src)
+    assert world.num_triangles == 100000 and world.num_spheres == 100
+    out, gst = world.render(w, h, spp, 8, mode=R.RNG_COUNTER)
+    assert_bits_equal(out, img, "mesh frame")
+    assert gst["rays"] == st["rays"] and gst["tri_in_range"] == st["tri_in_range"]
+
+
+def test_move_camera_then_render():
+    src = scene_text(CWORLD)
+    world = R.World(src)
+    ref = O.Scene(src)
+    for d in [(0.1, 0.0, 0.0), (0.0, -0.2, 0.5), (-0.3, 0.1, 0.2)]:
+        world.move_camera(*d)
+        cam = np.zeros(12, np.float32)
+        O.lib().ro_camera_move(O.fptr(ref.camera()), d[0], d[1], d[2], O.fptr(cam))
+        ref.set_camera(cam)
+        assert_bits_equal(world.camera(), ref.camera(), "camera")
+        img, _, _ = ref.render(32, 24, 4, 8, mode=O.RNG_COUNTER)
+        out, _ = world.render(32, 24, 4, 8, mode=R.RNG_COUNTER)
+        assert_bits_equal(out, img, "moved frame")
+
+
+def test_tiles_assemble_to_full_frame():
+    src = scene_text("rtow.txt")
+    world = R.World(src)
+    w, h, spp = 80, 45, 4
+    full, fst = world.render(w, h, spp, 8)
+    for nranks, block in [(2, 1), (3, 4), (8, 2)]:
+        rays = 0
+        asm = np.zeros_like(full)
+        for rank in range(nranks):
+            tile, st = world.render(w, h, spp, 8, row_block=block, rank=rank, nranks=nranks)
+            rays += st["rays"]
+            for k in range(tile.shape[0]):
+                asm[R.tile_row(k, block, rank, nranks)] = tile[k]
+        assert_bits_equal(asm, full, f"tiles {nranks}x{block}")
+        assert rays == fst["rays"]
+
+
+def test_slabs_do_not_change_the_frame(monkeypatch):
+    src = scene_text("rtow.txt")
+    w, h, spp = 50, 20, 8
+    one, _ = R.World(src).render(w, h, spp, 8)
+    monkeypatch.setenv("RT_AMD_SLAB_JOBS", str(w * spp * 3))  # 3 rows per launch
+    many, st = R.World(src).render(w, h, spp, 8)
+    assert st["trace_launches"] == 7
+    assert_bits_equal(many, one, "slabbed frame")
+
+
+def test_full_size_c2_properties():
+    """BASELINE configs[1] at full size: determinism + oracle parity on rows."""
+    src = S.rtow()
+    world = R.World(src)
+    W, H, spp, depth = 1920, 1080, 64, 8
+    a, st = world.render(W, H, spp, depth)
+    b, st2 = world.render(W, H, spp, depth)
+    assert_bits_equal(a, b, "determinism")
+    assert st["rays"] == st2["rays"] and st["samples"] == W * H * spp
+    assert (a[..., 3] == 255).all()
+    ref = O.Scene(src)
+    rows = [0, 333, 700, 1079]  # reference rows (0 = bottom)
+    img = np.zeros((H, W, 4), np.uint8)
+    for r in rows:
+        ref.render(W, H, spp, depth, mode=O.RNG_COUNTER, row_begin=r, row_step=H, nthreads=8,
+                   out=img)
+        assert_bits_equal(a[H - 1 - r], img[H - 1 - r], f"row {r}")
