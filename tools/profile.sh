@@ -1,0 +1,23 @@
+#!/bin/bash
+# rocprofv3 evidence for bench.py: kernel trace + stats, then FETCH_SIZE and
+# WRITE_SIZE in separate --pmc passes (MI355X_MICROARCH.md, rocprofv3 PMC slots).
+# usage: tools/profile.sh <tag> [bench args...]
+TAG=${1:-r01}; shift
+REPO="${GRAFT_REPO_ROOT:-/root/repo}"
+OUT="$REPO/gpurun_out/prof_$TAG"
+mkdir -p "$OUT"
+cd /tmp && export TMPDIR=/tmp
+run() {  # run <name> <secs> <rocprof args...>
+    local name=$1 secs=$2; shift 2
+    timeout -k 10 "$secs" rocprofv3 "$@" -d "$OUT/$name" -o "$name" --output-format csv \
+        -- python3 "$REPO/bench.py" --no-cpu-baseline "${BENCH_ARGS[@]}" > "$OUT/$name.log" 2>&1
+    local rc=$?
+    echo "$name rc=$rc"; tail -2 "$OUT/$name.log"
+    [ $rc -eq 0 ] || exit $rc
+}
+BENCH_ARGS=("$@")
+run trace 600 --kernel-trace --stats
+run pmc_fetch 600 --kernel-trace --pmc FETCH_SIZE
+run pmc_write 600 --kernel-trace --pmc WRITE_SIZE
+run pmc_valu 600 --kernel-trace --pmc SQ_INSTS_VALU SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE
+find "$OUT" -name "*.csv" | head -20
