@@ -32,6 +32,7 @@ import torch.distributed as dist  # noqa: E402
 
 import raytracer_amd as R  # noqa: E402
 import scenes as S  # noqa: E402
+import tiles  # noqa: E402
 
 METRIC = "Mrays/sec + frames/sec at 1920×1080 spp=64; 1/2/4/8 MI355X"
 FP32_VECTOR_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md, chip-level parameters
@@ -102,7 +103,7 @@ def main():
         st = world.render_device(W, H, tile.data_ptr(), stream.cuda_stream, spp=spp, depth=depth,
                                  row_block=ROW_BLOCK, rank=rank, nranks=nr, device=local_rank)
         if nr > 1:
-            dist.all_gather_into_tensor(gathered, tile)  # RCCL over xGMI
+            tiles.gather(tile, gathered)  # RCCL all-gather over xGMI
         return st
 
     for _ in range(args.warmup):

@@ -77,8 +77,9 @@ int rt_render_device(const Rust_WorldHandle *handle, size_t width, size_t height
 
 /* Diagnostics: copies the per-sample colours (r, g, b, 0 as 4 f32) of the
  * LAST trace launch on `device` (-1 = current) to host `out` (n floats max).
- * Job order = tile pixel-major, sample-minor: job = (k*width + col)*spp + s
- * for tile row k.  Returns the number of floats copied or a negative error. */
+ * Slab order is sample-major: slot = s*(rows*width) + k*width + col for
+ * sample s of tile row k (rows = tile rows of that launch).  Returns the
+ * number of floats copied or a negative error. */
 long rt_read_samples(const Rust_WorldHandle *handle, int device, float *out, size_t n);
 
 /* Frees a handle from load_world (the reference never frees, lib.rs:42-45). */

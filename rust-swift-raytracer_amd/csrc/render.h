@@ -30,6 +30,7 @@ struct TraceParams {
     uint32_t row_block, rank, nranks;
     uint32_t slab_row0;       // first tile row of this launch
     uint32_t njobs;           // samples in this launch
+    uint32_t npix;            // pixels in this launch (slab index = s*npix + pixel)
     uint32_t chunk;           // jobs fetched per atomic by one wave
 };
 

@@ -105,7 +105,7 @@ __global__ __launch_bounds__(256) void trace_kernel(TraceParams p) {
 
     F3 org = f3(0, 0, 0), dir = f3(0, 0, 0);
     float thr_r = 1.0f, thr_g = 1.0f, thr_b = 1.0f;  // ray_color's final_color
-    uint32_t rng = 0, job = 0, bounce = 0;
+    uint32_t rng = 0, slot = 0, bounce = 0;
     bool active = false;
     uint32_t rays = 0, tri_in = 0;
 
@@ -131,10 +131,11 @@ __global__ __launch_bounds__(256) void trace_kernel(TraceParams p) {
             const uint32_t rank = __builtin_amdgcn_mbcnt_hi(
                 (uint32_t)(dead >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)dead, 0u));
             if (!active && rank < avail) {
-                job = pool_next + rank;
+                const uint32_t job = pool_next + rank;
                 // job -> (tile row, column, sample) -> reference (row, col)
                 const uint32_t lp = job / p.spp;
                 const uint32_t s = job - lp * p.spp;
+                slot = s * p.npix + lp;  // sample-major slab: resolve reads coalesce
                 const uint32_t q = lp / p.width;
                 const uint32_t col = lp - q * p.width;
                 const uint32_t lr = p.slab_row0 + q;
@@ -293,7 +294,7 @@ __global__ __launch_bounds__(256) void trace_kernel(TraceParams p) {
             }
         }
         if (done) {
-            p.samples[job] = make_float4(out_r, out_g, out_b, 0.0f);
+            p.samples[slot] = make_float4(out_r, out_g, out_b, 0.0f);
             active = false;
         }
     }
@@ -311,7 +312,8 @@ __global__ __launch_bounds__(256) void trace_kernel(TraceParams p) {
 }
 
 // ------------------------------------------------------------ resolve kernel
-// Sums each pixel's samples in order (common.rs:333-341), gamma + `as u8`
+// Sums each pixel's samples in order (common.rs:333-341; slab is sample-major,
+// so consecutive threads read consecutive 16-B words), gamma + `as u8`
 // (:344-356), one RGBA8 word per pixel, coalesced along the row.
 __global__ __launch_bounds__(256) void resolve_kernel(const float4 *__restrict__ samples,
                                                       uint32_t *__restrict__ out, uint32_t npix,
@@ -320,9 +322,8 @@ __global__ __launch_bounds__(256) void resolve_kernel(const float4 *__restrict__
     const uint32_t lp = blockIdx.x * blockDim.x + threadIdx.x;
     if (lp >= npix) return;
     float r = 0.0f, g = 0.0f, b = 0.0f, a = 1.0f;  // Color::new(0,0,0): alpha 1
-    const float4 *s = samples + (size_t)lp * spp;
     for (uint32_t k = 0; k < spp; ++k) {
-        const float4 c = s[k];
+        const float4 c = samples[(size_t)k * npix + lp];  // sample-major slab
         r = r + c.x;
         g = g + c.y;
         b = b + c.z;

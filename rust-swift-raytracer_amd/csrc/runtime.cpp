@@ -190,6 +190,7 @@ int render_frame(WorldState &w, const CameraModel &cam, size_t width, size_t hei
         const uint64_t njobs = rows * jobs_per_row;
         p.slab_row0 = (uint32_t)r0;
         p.njobs = (uint32_t)njobs;
+        p.npix = (uint32_t)(rows * width);
         HIP_TRY(hipEventRecord(d->ev[0], s));
         if (njobs) {
             uint64_t blocks = std::min<uint64_t>(full_blocks, (njobs + 1023) / 1024);

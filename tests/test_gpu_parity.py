@@ -25,9 +25,9 @@ CWORLD = "c_raytracer_world.txt"
 
 
 def oracle_samples_to_gpu_order(samples, width, height, spp):
-    """Oracle job = (row*W + col)*spp + s (row 0 = bottom); GPU tile order is
-    image row (top first) major."""
-    a = samples.reshape(height, width, spp, 4)[::-1]
+    """Oracle job = (row*W + col)*spp + s (row 0 = bottom); the GPU slab is
+    sample-major over image rows (top first): slot = s*(H*W) + ir*W + col."""
+    a = samples.reshape(height, width, spp, 4)[::-1].transpose(2, 0, 1, 3)
     return np.ascontiguousarray(a).reshape(-1, 4)
 
 

@@ -1,0 +1,104 @@
+"""CPU tests of the product scene parser (load_world, lib.rs:37-46 ->
+parser.rs:336-381) against the oracle's restatement of parser.rs.
+
+Every parsed float, camera vector and material must be bit-identical, and
+every rejected input must fail with the same ParseError kind (parser.rs:11-18;
+100 = an input on which the reference panics).  No GPU needed.
+"""
+import numpy as np
+import pytest
+
+import oracle as O
+import raytracer_amd as R
+import scenes as S
+from conftest import scene_text
+
+CAM = "camera origin 0.0 0.0 0.0 aspect 1.77778;\n"
+MAT = "material M : Diffuse color 0.5 0.25 0.125;\n"
+
+
+def parse_both(src):
+    try:
+        w = R.World(src)
+        perr = None
+    except ValueError:
+        w, perr = None, R.lib().rt_last_parse_error()
+    try:
+        s = O.Scene(src)
+        oerr = None
+    except ValueError:
+        s, oerr = None, O.lib().ro_last_parse_error()
+    return w, perr, s, oerr
+
+
+def assert_same_scene(w, s):
+    assert w.num_spheres == s.num_spheres and w.num_triangles == s.num_triangles
+    assert np.array_equal(w.camera().view(np.uint32), s.camera().view(np.uint32))
+    assert np.array_equal(w.spheres().view(np.uint32), s.spheres().view(np.uint32))
+    assert np.array_equal(w.triangles().view(np.uint32), s.triangles().view(np.uint32))
+
+
+@pytest.mark.parametrize("src", [
+    scene_text("world.txt"), scene_text("c_raytracer_world.txt"), S.three_spheres(), S.rtow(),
+    CAM,
+    "cameraorigin0.0 0.0 0.0aspect 1.0;",                  # keywords need no whitespace
+    "camera origin 0.0 0.0 0.0 aspect 1.0;\n  // comment after whitespace\n",
+    "camera origin 0 0 0 aspect 1;\n",                      # integer literals
+    "camera origin .5 5. -0.0 aspect 2.;\n",                # Rust accepts .5 and 5.
+    "// leading comment\n" + CAM + "// c\n" + MAT + "sphere center 0.0 0.0 -1.0 radius 0.5 material M;",
+    CAM + MAT + "material M : Metal color 0.1 0.2 0.3 fuzz 0.4;\n"
+          "sphere center 0.0 0.0 -1.0 radius 0.5 material M;",  # duplicate name: last wins
+    CAM + "material a_1 : Dielectric ir 1.333333333333333333333;\n"
+          "triangle v0 -1.0 -1.0 -2.0 v1 1.0 -1.0 -2.0 v2 0.0 1.0 -2.0 material a_1;",
+    CAM + "material M : Diffuse color 0.1000000000000000055511151231257827 0.3 16777217.0;\n",
+    CAM + "material Mé : Diffuse color 1.0 1.0 1.0;\nsphere center 0.0 0.0 -1.0 radius 0.5 material Mé;",
+])
+def test_accepted_inputs_parse_identically(src):
+    w, perr, s, oerr = parse_both(src)
+    assert perr is None and oerr is None, (perr, oerr)
+    assert_same_scene(w, s)
+
+
+@pytest.mark.parametrize("src,kind", [
+    ("", 1),                                                     # MissingCamera
+    ("\n" + CAM, 1),                                             # skip_comment skips no whitespace
+    ("camera origin 0.0 0.0 0.0 aspect 1.0", 3),                 # no ';' after the last float
+    ("camera origin 0.0 0.0 0.0 aspect 1;", 5),                  # "1;" is only 2 bytes
+    ("camera origin 0.0 0.0 0.0 aspect 1.0 ", 3),                # missing ';'
+    ("camera origin 0.0 x 0.0 aspect 1.0;", 5),                  # NotAF32
+    ("camera origin 0.0 1.2.3 0.0 aspect 1.0;", 5),              # two dots
+    ("camera origin - 0.0 0.0 aspect 1.0;", 5),                  # lone sign
+    (CAM + "sphere center 0.0 0.0 -1.0 radius 0.5 material NOPE;", 2),
+    (CAM + MAT + "material X : Glass ir 1.5;", 2),
+    (CAM + "junk", 2),
+    (CAM + "// no newline at the end", 2),
+    (CAM + "sphere center 0.0 0.0 -1.0 radius 0.5 material M;\n" + MAT, 2),  # order matters
+    (CAM + "// commentaire é\n", 100),                          # non-ASCII in a comment panics
+])
+def test_rejected_inputs_fail_the_same_way(src, kind):
+    w, perr, s, oerr = parse_both(src)
+    assert w is None and s is None
+    assert perr == oerr == kind, (perr, oerr)
+
+
+def test_invalid_utf8_is_rejected():
+    w, perr, s, oerr = parse_both(CAM.encode() + b"// \xff\xfe\n")
+    assert w is None and s is None and perr == oerr == 100
+
+
+def test_mesh_scene_parses_identically():
+    src = S.mesh(nx=20, ny=10, nspheres=30)
+    w, perr, s, oerr = parse_both(src)
+    assert perr is None and oerr is None
+    assert_same_scene(w, s)
+
+
+def test_move_camera_matches_reference_formula():
+    w = R.World(scene_text("world.txt"))
+    s = O.Scene(scene_text("world.txt"))
+    for d in [(1.0, 0.5, -0.25), (0.1, 0.1, 0.1), (-3.0, 2.0, 7.5)]:
+        w.move_camera(*d)
+        cam = np.zeros(12, np.float32)
+        O.lib().ro_camera_move(O.fptr(s.camera()), d[0], d[1], d[2], O.fptr(cam))
+        s.set_camera(cam)
+        assert np.array_equal(w.camera().view(np.uint32), cam.view(np.uint32))

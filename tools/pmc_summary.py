@@ -1,0 +1,64 @@
+"""Summarise a tools/profile.sh output directory (rocprofv3 CSVs) into JSON.
+
+HBM bytes follow MI355X_MICROARCH.md §HBM: FETCH_SIZE and WRITE_SIZE are KB
+from separate --pmc passes; on gfx950 FETCH_SIZE reads 1/2 of the bytes of
+wide coalesced streaming reads, so fetched bytes are reported both raw and
+x2-corrected; WRITE_SIZE is exact for 16-B-per-lane stores.
+
+usage: python tools/pmc_summary.py gpurun_out/prof_r01 profiles/r01 [config]
+"""
+import collections
+import csv
+import glob
+import json
+import os
+import shutil
+import sys
+
+
+def short(name):
+    for k in ("trace_kernel", "resolve_kernel"):
+        if k in name:
+            return k
+    return name[:60]
+
+
+def main(src, dst, config="c2"):
+    os.makedirs(dst, exist_ok=True)
+    out = {"source": os.path.basename(src.rstrip("/")), "kernels": {}}
+    stats = glob.glob(os.path.join(src, "trace", "*kernel_stats.csv"))
+    if stats:
+        shutil.copy(stats[0], os.path.join(dst, "kernel_stats.csv"))
+        for r in csv.DictReader(open(stats[0])):
+            k = out["kernels"].setdefault(short(r["Name"]), {})
+            k["calls"] = int(r["Calls"])
+            k["avg_ns"] = float(r["AverageNs"])
+            k["pct_time"] = float(r["Percentage"])
+    for f in glob.glob(os.path.join(src, "pmc_*", "*counter_collection.csv")):
+        agg = collections.defaultdict(list)
+        for r in csv.DictReader(open(f)):
+            agg[(short(r["Kernel_Name"]), r["Counter_Name"])].append(float(r["Counter_Value"]))
+        for (kern, ctr), v in agg.items():
+            if kern in ("trace_kernel", "resolve_kernel"):
+                out["kernels"].setdefault(kern, {})[ctr] = sum(v) / len(v)
+    for k in out["kernels"].values():
+        if "FETCH_SIZE" in k and "WRITE_SIZE" in k:
+            k["hbm_fetch_bytes_raw"] = k["FETCH_SIZE"] * 1024
+            k["hbm_fetch_bytes_x2"] = 2 * k["FETCH_SIZE"] * 1024
+            k["hbm_write_bytes"] = k["WRITE_SIZE"] * 1024
+            k["hbm_bytes_per_launch"] = k["hbm_fetch_bytes_x2"] + k["hbm_write_bytes"]
+    with open(os.path.join(dst, "summary.json"), "w") as fh:
+        json.dump(out, fh, indent=1)
+    tr = out["kernels"].get("trace_kernel", {})
+    if "hbm_bytes_per_launch" in tr:
+        path = os.path.join(os.path.dirname(dst.rstrip("/")), "hbm_traffic.json")
+        allc = json.load(open(path)) if os.path.exists(path) else {}
+        allc[config] = {"trace_bytes_per_launch": tr["hbm_bytes_per_launch"],
+                        "from": os.path.relpath(dst, os.path.dirname(path))}
+        with open(path, "w") as fh:
+            json.dump(allc, fh, indent=1)
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main(*sys.argv[1:])
