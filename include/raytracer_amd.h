@@ -36,7 +36,14 @@ typedef struct RtRenderOptions {
   uint32_t rank;                  /* blocks of row_block rows, round-robin over */
   uint32_t nranks;                /* nranks; this call renders rank's rows      */
   int32_t device;                 /* HIP device ordinal, -1 = current device    */
+  int32_t accel;                  /* RT_ACCEL_*: how World::hit finds spheres   */
 } RtRenderOptions;
+
+/* Sphere search.  Both give bit-identical frames:
+ *   RT_ACCEL_BRUTE: every sphere in file order (common.rs:241-247).
+ *   RT_ACCEL_BVH:   exact-pruning BVH (falls back to BRUTE for < 16 spheres).
+ *   RT_ACCEL_AUTO:  BVH when the scene has one, else BRUTE.  Default. */
+enum { RT_ACCEL_AUTO = 0, RT_ACCEL_BRUTE = 1, RT_ACCEL_BVH = 2 };
 
 typedef struct RtRenderStats {
   uint64_t samples;        /* pixel samples traced                           */
@@ -48,6 +55,10 @@ typedef struct RtRenderStats {
   double resolve_ms;       /* HIP-event time of the resolve kernel(s)        */
   uint32_t trace_launches; /* number of trace launches (slabs)               */
   uint32_t waves;          /* persistent waves per trace launch              */
+  uint32_t accel;          /* RT_ACCEL_BRUTE or RT_ACCEL_BVH (what ran)      */
+  uint64_t bvh_sphere_tests; /* sphere tests executed inside the BVH         */
+  uint64_t bvh_node_tests;   /* BVH node (box) tests executed                */
+  uint64_t big_sphere_tests; /* rays * spheres kept out of the BVH           */
 } RtRenderStats;
 
 /* spp 16, depth 8 (lib.rs:51), COUNTER, seed 2547549, one rank, device -1. */

@@ -1,0 +1,43 @@
+// bvh.h -- exact-pruning sphere BVH (host build, device layout).
+//
+// The reference tests every sphere in file order with a shrinking t_max
+// (common.rs:241-247).  A sphere's *candidate* root -- root1 if root1 > t_min,
+// else root2 if root2 > t_min (common.rs:84-92) -- does not depend on t_max,
+// and the reference keeps the smallest candidate, first index winning ties.
+// So any visiting order that (1) applies the same candidate arithmetic and
+// (2) keeps the argmin with an (t, index) tie-break returns the identical
+// sphere and t.  Pruning is exact because the point o + t*d of any computed
+// candidate lies within  r + K*(|o - c| + r)  of the centre (rounding-error
+// bound), so a box inflated by that margin per ray can never
+// hide a sphere the brute-force loop would accept.
+#pragma once
+
+#include <cstdint>
+#include <vector>
+
+#include "scene.h"
+
+namespace rtamd {
+
+// Nodes: two float4 each.  lo = (min.x, min.y, min.z, bits(a)), hi = (max.x,
+// max.y, max.z, bits(b)).  Internal: a = left child index (right = a + 1),
+// b = split axis.  Leaf: a = first primitive | kLeafBit, b = primitive count.
+constexpr uint32_t kLeafBit = 0x80000000u;
+constexpr uint32_t kNodeEnd = 0xFFFFFFFFu;
+
+struct SphereBVH {
+    std::vector<float> nodes;       // 8 floats per node
+    std::vector<uint32_t> miss;     // 8 per node: DFS successor per ray octant
+    std::vector<float> prims;       // 4 floats per BVH sphere: (cx, cy, cz, r*r)
+    std::vector<uint32_t> prim_id;  // original sphere index (tie-break, shading)
+    std::vector<uint32_t> big;      // spheres always tested by brute force (ascending)
+    // Per-ray inflation inputs (all rounded up): |o - c| <= |o - centre| + radius
+    // for every BVH sphere; rmax = largest BVH radius; mag = largest |coordinate|.
+    float centre[3] = {0, 0, 0};
+    float radius = 0, rmax = 0, mag = 0;
+    uint32_t depth = 0;
+};
+
+SphereBVH build_sphere_bvh(const std::vector<Sphere> &spheres, uint32_t leaf_size);
+
+}  // namespace rtamd

@@ -48,6 +48,7 @@ Rust_WorldHandle *load_world(const char *source) {
     }
     // spheres padded to the kernel's scalar-load batch of 8 with NaN centres
     world->state.packed = rtamd::pack_scene(world->state.scene, 8, 1);
+    world->state.bvh = rtamd::build_sphere_bvh(world->state.scene.spheres, 2);
     auto *cam = new Rust_Camera{world->state.scene.camera};
     return new Rust_WorldHandle{world, cam};
 }
@@ -82,6 +83,7 @@ void rt_default_options(RtRenderOptions *o) {
     o->rank = 0;
     o->nranks = 1;
     o->device = -1;
+    o->accel = RT_ACCEL_AUTO;
 }
 
 size_t rt_tile_rows(size_t height, uint32_t row_block, uint32_t rank, uint32_t nranks) {

@@ -19,7 +19,7 @@ struct TraceParams {
     const float *mats;        // 8 floats per material: kind bits, r, g, b, param
     float4 *samples;          // slab-local per-sample colour (r, g, b, 0)
     uint32_t *job_counter;    // zeroed before every launch
-    unsigned long long *stats;// [0] rays, [1] triangle tests in t-range
+    unsigned long long *stats;// rays, tri in t-range, BVH sphere tests, BVH node tests
     const uint32_t *replay;   // REPLAY start states (global job index)
     float cam[12];            // origin, lower_left, horizontal, vertical
     float wden, hden;         // (width-1) as f32, (height-1) as f32
@@ -32,6 +32,15 @@ struct TraceParams {
     uint32_t njobs;           // samples in this launch
     uint32_t npix;            // pixels in this launch (slab index = s*npix + pixel)
     uint32_t chunk;           // jobs fetched per atomic by one wave
+    // exact-pruning BVH (bvh.h); nnodes == 0 selects the brute-force kernel
+    const float4 *bvh_nodes;  // 2 per node
+    const uint32_t *bvh_miss; // 8 per node (one DFS successor per ray octant)
+    const float4 *bvh_prims;  // (cx, cy, cz, r*r) in BVH order
+    const uint32_t *bvh_prim_id;
+    const float4 *big_hot;    // spheres kept out of the tree (tested first)
+    const uint32_t *big_id;
+    uint32_t nnodes, nbig;
+    float bvh_c[3], bvh_r, bvh_rmax, bvh_mag;
 };
 
 hipError_t launch_trace(const TraceParams &p, uint32_t blocks, hipStream_t stream);
@@ -39,6 +48,6 @@ hipError_t launch_trace(const TraceParams &p, uint32_t blocks, hipStream_t strea
 hipError_t launch_resolve_ex(const float4 *samples, uint32_t *out, uint32_t npix, uint32_t spp,
                              float inv_spp, uint32_t width, uint32_t slab_row0,
                              hipStream_t stream);
-hipError_t trace_occupancy(int *blocks_per_cu);
+hipError_t trace_occupancy(int *blocks_per_cu, bool bvh);
 
 }  // namespace rtamd

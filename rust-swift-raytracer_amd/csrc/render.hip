@@ -96,9 +96,142 @@ __device__ __forceinline__ float4 uniform_load(const float4 *base, uint32_t i) {
 }
 
 constexpr uint32_t kWave = 64;
+constexpr uint32_t kNodeEndDev = 0xFFFFFFFFu;  // bvh.h kNodeEnd
+constexpr uint32_t kLeafBitDev = 0x80000000u;  // bvh.h kLeafBit
 constexpr uint32_t kBatch = 8;  // spheres per scalar-load batch (sphere count padded to it)
 
+// ------------------------------------------------------------ sphere stage
+// Brute force, file order, shrinking t_max (common.rs:241-247).  Batches of
+// kBatch spheres: all scalar loads issue up front, the discriminants
+// (independent of t_max) are computed for the whole batch, and the in-order
+// root/t_max updates run only when some lane's discriminant is non-negative
+// (rare; wave-uniform skip).
+__device__ __forceinline__ void spheres_brute(const TraceParams &p, F3 org, F3 dir, float &best_t,
+                                              int &best_i) {
+    const float tmin = 0.001f;
+    for (uint32_t i0 = 0; i0 < p.nsph_padded; i0 += kBatch) {
+        float hb[kBatch], disc[kBatch];
+        bool any = false;
+#pragma unroll
+        for (uint32_t k = 0; k < kBatch; ++k) {
+            const float4 S = uniform_load(p.sph_hot, i0 + k);
+            const float ocx = org.x - S.x, ocy = org.y - S.y, ocz = org.z - S.z;
+            hb[k] = (ocx * dir.x + ocy * dir.y) + ocz * dir.z;
+            const float cc = ((ocx * ocx + ocy * ocy) + ocz * ocz) - S.w;
+            disc[k] = hb[k] * hb[k] - cc;  // a == 1.0 exactly (maths.rs:127)
+            any |= disc[k] >= 0.0f;
+        }
+        if (!any) continue;
+#pragma unroll
+        for (uint32_t k = 0; k < kBatch; ++k) {
+            if (disc[k] >= 0.0f) {
+                const float sq = __builtin_sqrtf(disc[k]);
+                const float r1 = -hb[k] - sq;
+                const float r2 = -hb[k] + sq;
+                const bool ok1 = (tmin < r1) && (r1 < best_t);
+                const bool ok2 = (tmin < r2) && (r2 < best_t);
+                if (ok1 || ok2) {
+                    best_t = ok1 ? r1 : r2;  // r1 <= r2: the smaller valid root
+                    best_i = (int)(i0 + k);
+                }
+            }
+        }
+    }
+}
+
+// One sphere in any order: same arithmetic as Sphere::hit (common.rs:74-92);
+// the candidate (root1 if > t_min, else root2 if > t_min) is independent of
+// t_max, and the reference keeps the smallest candidate, lowest index first.
+__device__ __forceinline__ bool sphere_candidate(float4 S, F3 org, F3 dir, int idx, float &best_t,
+                                                 int &best_i) {
+    const float tmin = 0.001f;
+    const float ocx = org.x - S.x, ocy = org.y - S.y, ocz = org.z - S.z;
+    const float hb = (ocx * dir.x + ocy * dir.y) + ocz * dir.z;
+    const float cc = ((ocx * ocx + ocy * ocy) + ocz * ocz) - S.w;
+    const float disc = hb * hb - cc;
+    if (!(disc >= 0.0f)) return false;
+    const float sq = __builtin_sqrtf(disc);
+    const float r1 = -hb - sq;
+    const float r2 = -hb + sq;
+    const bool v1 = tmin < r1;
+    const float c = v1 ? r1 : r2;
+    const bool valid = v1 || (tmin < r2);
+    const bool take = valid && (c < best_t || (c == best_t && best_t < __builtin_inff() && idx < best_i));
+    if (take) { best_t = c; best_i = idx; }
+    return take;
+}
+
+// Slab bounds widened by 1e-6 relative (covers the ~3 ulp error of the slab
+// arithmetic) so that a box is only pruned when it is certainly missed.
+__device__ __forceinline__ float lower_rel(float x) { return x * (x > 0.0f ? 0.999999f : 1.000001f); }
+__device__ __forceinline__ float upper_rel(float x) { return x * (x > 0.0f ? 1.000001f : 0.999999f); }
+
+constexpr float kErrK = 3.0e-3f;  // >= 2.7x the derived sqrt(30u) = 1.12e-3
+
+// Spheres through the exact-pruning BVH (bvh.h).  Big spheres first (brute
+// force, wave-uniform), then a stackless octant-ordered traversal: every
+// node box is inflated per ray by e = K*(min(A, best_t + R)*(1+3K) + R) + e_abs,
+// which bounds how far a computed candidate's point can lie outside its
+// sphere; a node is skipped only when the inflated box is certainly missed
+// or certainly starts beyond best_t.
+__device__ __forceinline__ void spheres_bvh(const TraceParams &p, F3 org, F3 dir, float &best_t,
+                                            int &best_i, uint32_t &sph_tests,
+                                            uint32_t &node_tests) {
+    for (uint32_t k = 0; k < p.nbig; ++k) {
+        const float4 S = uniform_load(p.big_hot, k);
+        const int idx = (int)p.big_id[k];
+        sphere_candidate(S, org, dir, idx, best_t, best_i);
+    }
+    if (p.nnodes == 0) return;
+    const float ix = 1.0f / dir.x, iy = 1.0f / dir.y, iz = 1.0f / dir.z;
+    const uint32_t oct = (ix < 0.0f ? 1u : 0u) | (iy < 0.0f ? 2u : 0u) | (iz < 0.0f ? 4u : 0u);
+    const float ax = org.x - p.bvh_c[0], ay = org.y - p.bvh_c[1], az = org.z - p.bvh_c[2];
+    const float A = __builtin_sqrtf((ax * ax + ay * ay) + az * az) * 1.00001f + p.bvh_r;
+    const float e_abs = 2e-6f * ((fabsf(org.x) + fabsf(org.y)) + fabsf(org.z) + p.bvh_mag);
+    auto inflation = [&](float bt) {
+        const float a = fminf(A, bt + p.bvh_rmax);  // fminf(A, inf) = A
+        return kErrK * (a * (1.0f + 3.0f * kErrK) + p.bvh_rmax) + e_abs;
+    };
+    float e = inflation(best_t);
+    F3 lo = f3(org.x + e, org.y + e, org.z + e);  // (bmin - e) - o == bmin - (o + e)
+    F3 hi = f3(org.x - e, org.y - e, org.z - e);
+    uint32_t node = 0;
+    while (node != kNodeEndDev) {
+        ++node_tests;
+        const float4 B0 = p.bvh_nodes[2 * node];
+        const float4 B1 = p.bvh_nodes[2 * node + 1];
+        const float t0x = (B0.x - lo.x) * ix, t1x = (B1.x - hi.x) * ix;
+        const float t0y = (B0.y - lo.y) * iy, t1y = (B1.y - hi.y) * iy;
+        const float t0z = (B0.z - lo.z) * iz, t1z = (B1.z - hi.z) * iz;
+        const float tn = fmaxf(fmaxf(fminf(t0x, t1x), fminf(t0y, t1y)), fminf(t0z, t1z));
+        const float tf = fminf(fminf(fmaxf(t0x, t1x), fmaxf(t0y, t1y)), fmaxf(t0z, t1z));
+        const bool skip = lower_rel(tn) > upper_rel(tf) || upper_rel(tf) < 0.001f ||
+                          lower_rel(tn) > upper_rel(best_t);
+        const uint32_t a = __float_as_uint(B0.w);
+        if (skip) {
+            node = p.bvh_miss[8 * node + oct];
+        } else if (a & kLeafBitDev) {
+            const uint32_t first = a & ~kLeafBitDev, count = __float_as_uint(B1.w);
+            bool changed = false;
+            for (uint32_t j = first; j < first + count; ++j) {
+                ++sph_tests;
+                changed |= sphere_candidate(p.bvh_prims[j], org, dir, (int)p.bvh_prim_id[j], best_t,
+                                            best_i);
+            }
+            if (changed) {
+                e = inflation(best_t);
+                lo = f3(org.x + e, org.y + e, org.z + e);
+                hi = f3(org.x - e, org.y - e, org.z - e);
+            }
+            node = p.bvh_miss[8 * node + oct];
+        } else {
+            node = a + ((oct >> __float_as_uint(B1.w)) & 1u);  // near child first
+        }
+    }
+}
+
 // ------------------------------------------------------------ trace kernel
+template <bool kBvh>
 __global__ __launch_bounds__(256) void trace_kernel(TraceParams p) {
     const uint32_t lane = __lane_id();
     const float tmin = 0.001f;                 // common.rs:242, 250
@@ -107,7 +240,7 @@ __global__ __launch_bounds__(256) void trace_kernel(TraceParams p) {
     float thr_r = 1.0f, thr_g = 1.0f, thr_b = 1.0f;  // ray_color's final_color
     uint32_t rng = 0, slot = 0, bounce = 0;
     bool active = false;
-    uint32_t rays = 0, tri_in = 0;
+    uint32_t rays = 0, tri_in = 0, sph_tests = 0, node_tests = 0;
 
     uint32_t pool_next = 0, pool_end = 0;  // wave-uniform job pool
     bool exhausted = false;
@@ -172,39 +305,12 @@ __global__ __launch_bounds__(256) void trace_kernel(TraceParams p) {
         } else {
             ++rays;
             // World::hit, spheres in order with shrinking t_max (common.rs:241-247)
-            // Batches of kBatch spheres: all scalar loads issue up front, the
-            // discriminants (independent of t_max) are computed for the whole
-            // batch, and the in-order root/t_max updates run only when some
-            // lane's discriminant is non-negative (rare; wave-uniform skip).
             float best_t = __builtin_inff();
             int best_i = -1;
-            for (uint32_t i0 = 0; i0 < p.nsph_padded; i0 += kBatch) {
-                float hb[kBatch], disc[kBatch];
-                bool any = false;
-#pragma unroll
-                for (uint32_t k = 0; k < kBatch; ++k) {
-                    const float4 S = uniform_load(p.sph_hot, i0 + k);
-                    const float ocx = org.x - S.x, ocy = org.y - S.y, ocz = org.z - S.z;
-                    hb[k] = (ocx * dir.x + ocy * dir.y) + ocz * dir.z;
-                    const float cc = ((ocx * ocx + ocy * ocy) + ocz * ocz) - S.w;
-                    disc[k] = hb[k] * hb[k] - cc;  // a == 1.0 exactly (maths.rs:127)
-                    any |= disc[k] >= 0.0f;
-                }
-                if (!any) continue;
-#pragma unroll
-                for (uint32_t k = 0; k < kBatch; ++k) {
-                    if (disc[k] >= 0.0f) {
-                        const float sq = __builtin_sqrtf(disc[k]);
-                        const float r1 = -hb[k] - sq;
-                        const float r2 = -hb[k] + sq;
-                        const bool ok1 = (tmin < r1) && (r1 < best_t);
-                        const bool ok2 = (tmin < r2) && (r2 < best_t);
-                        if (ok1 || ok2) {
-                            best_t = ok1 ? r1 : r2;  // r1 <= r2: the smaller valid root
-                            best_i = (int)(i0 + k);
-                        }
-                    }
-                }
+            if (kBvh) {
+                spheres_bvh(p, org, dir, best_t, best_i, sph_tests, node_tests);
+            } else {
+                spheres_brute(p, org, dir, best_t, best_i);
             }
             // Mesh::hit with t_max = best_t, own closest from +inf (common.rs:178-223)
             float tri_t = __builtin_inff();
@@ -300,14 +406,14 @@ __global__ __launch_bounds__(256) void trace_kernel(TraceParams p) {
     }
 
     // ---- per-wave statistics: one atomic per counter per wave ------------
-    uint64_t r = rays, ti = tri_in;
-    for (uint32_t off = kWave / 2; off > 0; off >>= 1) {
-        r += __shfl_xor(r, (int)off);
-        ti += __shfl_xor(ti, (int)off);
-    }
+    uint64_t c[4] = {rays, tri_in, sph_tests, node_tests};
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+        for (uint32_t off = kWave / 2; off > 0; off >>= 1) c[k] += __shfl_xor(c[k], (int)off);
     if (lane == 0) {
-        atomicAdd(&p.stats[0], (unsigned long long)r);
-        atomicAdd(&p.stats[1], (unsigned long long)ti);
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            if (c[k]) atomicAdd(&p.stats[k], (unsigned long long)c[k]);
     }
 }
 
@@ -341,7 +447,10 @@ __global__ __launch_bounds__(256) void resolve_kernel(const float4 *__restrict__
 }  // namespace
 
 hipError_t launch_trace(const TraceParams &p, uint32_t blocks, hipStream_t stream) {
-    hipLaunchKernelGGL(trace_kernel, dim3(blocks), dim3(256), 0, stream, p);
+    if (p.nnodes)
+        hipLaunchKernelGGL(trace_kernel<true>, dim3(blocks), dim3(256), 0, stream, p);
+    else
+        hipLaunchKernelGGL(trace_kernel<false>, dim3(blocks), dim3(256), 0, stream, p);
     return hipGetLastError();
 }
 
@@ -354,8 +463,9 @@ hipError_t launch_resolve_ex(const float4 *samples, uint32_t *out, uint32_t npix
     return hipGetLastError();
 }
 
-hipError_t trace_occupancy(int *blocks_per_cu) {
-    return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, trace_kernel, 256, 0);
+hipError_t trace_occupancy(int *blocks_per_cu, bool bvh) {
+    if (bvh) return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, trace_kernel<true>, 256, 0);
+    return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, trace_kernel<false>, 256, 0);
 }
 
 }  // namespace rtamd

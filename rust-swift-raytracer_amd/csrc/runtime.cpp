@@ -43,7 +43,8 @@ const std::string &last_error() { return g_error; }
 DeviceState::~DeviceState() {
     if (device < 0) return;
     if (hipSetDevice(device) != hipSuccess) return;
-    void *bufs[] = {sph_hot, sph_cold, tri_hot, tri_geo, mats, samples, out, replay, counter, stats};
+    void *bufs[] = {sph_hot, sph_cold, tri_hot, tri_geo, mats, samples, out, replay, counter, stats,
+                    bvh_nodes, bvh_prims, big_hot, bvh_miss, bvh_prim_id, big_id};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
     for (hipEvent_t e : ev)
@@ -88,10 +89,12 @@ static int device_for(WorldState &w, int want, DeviceState *&out) {
         hipDeviceProp_t prop;
         HIP_TRY(hipGetDeviceProperties(&prop, dev));
         d->num_cus = prop.multiProcessorCount;
-        HIP_TRY(trace_occupancy(&d->blocks_per_cu));
+        HIP_TRY(trace_occupancy(&d->blocks_per_cu, false));
+        HIP_TRY(trace_occupancy(&d->blocks_per_cu_bvh, true));
         const uint64_t bpc = env_u64("RT_AMD_BLOCKS_PER_CU", 0);
-        if (bpc) d->blocks_per_cu = (int)bpc;
+        if (bpc) d->blocks_per_cu = d->blocks_per_cu_bvh = (int)bpc;
         if (d->blocks_per_cu < 1) d->blocks_per_cu = 1;
+        if (d->blocks_per_cu_bvh < 1) d->blocks_per_cu_bvh = 1;
         // scene upload (once per device)
         const PackedScene &p = w.packed;
         auto up = [&](void **dst, const std::vector<float> &src) -> hipError_t {
@@ -107,6 +110,26 @@ static int device_for(WorldState &w, int want, DeviceState *&out) {
         d->nsph = p.nsph;
         d->nsph_padded = p.nsph_padded;
         d->ntri = p.ntri;
+        const SphereBVH &bv = w.bvh;
+        if (!bv.nodes.empty()) {
+            auto upu = [&](void **dst, const std::vector<uint32_t> &src) -> hipError_t {
+                hipError_t e = hipMalloc(dst, std::max<size_t>(src.size(), 1) * sizeof(uint32_t));
+                if (e != hipSuccess || src.empty()) return e;
+                return hipMemcpy(*dst, src.data(), src.size() * sizeof(uint32_t), hipMemcpyHostToDevice);
+            };
+            std::vector<float> big_hot;
+            for (uint32_t i : bv.big)
+                for (int k = 0; k < 4; ++k) big_hot.push_back(p.sph_hot[(size_t)i * 4 + k]);
+            if (big_hot.empty()) big_hot.assign(4, 0.0f);
+            HIP_TRY(up((void **)&d->bvh_nodes, bv.nodes));
+            HIP_TRY(up((void **)&d->bvh_prims, bv.prims));
+            HIP_TRY(up((void **)&d->big_hot, big_hot));
+            HIP_TRY(upu((void **)&d->bvh_miss, bv.miss));
+            HIP_TRY(upu((void **)&d->bvh_prim_id, bv.prim_id));
+            HIP_TRY(upu((void **)&d->big_id, bv.big));
+            d->nnodes = (uint32_t)(bv.nodes.size() / 8);
+            d->nbig = (uint32_t)bv.big.size();
+        }
         HIP_TRY(hipMalloc((void **)&d->counter, 64));
         HIP_TRY(hipMalloc((void **)&d->stats, 64));
         slot = std::move(d);
@@ -161,7 +184,7 @@ int render_frame(WorldState &w, const CameraModel &cam, size_t width, size_t hei
         HIP_TRY(grow(d->replay, d->replay_cap, n));
         HIP_TRY(hipMemcpyAsync(d->replay, o.replay_states, n * 4, hipMemcpyHostToDevice, s));
     }
-    HIP_TRY(hipMemsetAsync(d->stats, 0, 16, s));
+    HIP_TRY(hipMemsetAsync(d->stats, 0, 32, s));
 
     TraceParams p{};
     p.sph_hot = d->sph_hot; p.sph_cold = d->sph_cold;
@@ -180,9 +203,20 @@ int render_frame(WorldState &w, const CameraModel &cam, size_t width, size_t hei
     p.depth = o.max_ray_bounces;
     p.mode = o.rng_mode; p.seed = o.seed;
     p.row_block = B; p.rank = o.rank; p.nranks = nranks;
+    const bool use_bvh = d->nnodes > 0 && o.accel != RT_ACCEL_BRUTE;
+    if (use_bvh) {
+        const SphereBVH &bv = w.bvh;
+        p.bvh_nodes = d->bvh_nodes; p.bvh_miss = d->bvh_miss;
+        p.bvh_prims = d->bvh_prims; p.bvh_prim_id = d->bvh_prim_id;
+        p.big_hot = d->big_hot; p.big_id = d->big_id;
+        p.nnodes = d->nnodes; p.nbig = d->nbig;
+        for (int k = 0; k < 3; ++k) p.bvh_c[k] = bv.centre[k];
+        p.bvh_r = bv.radius; p.bvh_rmax = bv.rmax; p.bvh_mag = bv.mag;
+    }
     const float inv_spp = 1.0f / (float)o.samples_per_pixel;  // 1.0 / spp as f32 (common.rs:345)
 
-    const uint64_t full_blocks = (uint64_t)d->blocks_per_cu * (uint64_t)d->num_cus;
+    const uint64_t full_blocks =
+        (uint64_t)(use_bvh ? d->blocks_per_cu_bvh : d->blocks_per_cu) * (uint64_t)d->num_cus;
     double trace_ms = 0.0, resolve_ms = 0.0;
     uint32_t launches = 0, waves = 0;
     for (size_t r0 = 0; r0 < T; r0 += rows_per_slab) {
@@ -216,8 +250,8 @@ int render_frame(WorldState &w, const CameraModel &cam, size_t width, size_t hei
         trace_ms += a;
         resolve_ms += b;
     }
-    unsigned long long st[2] = {0, 0};
-    HIP_TRY(hipMemcpyAsync(st, d->stats, 16, hipMemcpyDeviceToHost, s));
+    unsigned long long st[4] = {0, 0, 0, 0};
+    HIP_TRY(hipMemcpyAsync(st, d->stats, 32, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
     if (stats) {
         stats->samples = (uint64_t)T * jobs_per_row;
@@ -229,6 +263,10 @@ int render_frame(WorldState &w, const CameraModel &cam, size_t width, size_t hei
         stats->resolve_ms = resolve_ms;
         stats->trace_launches = launches;
         stats->waves = waves;
+        stats->accel = use_bvh ? RT_ACCEL_BVH : RT_ACCEL_BRUTE;
+        stats->bvh_sphere_tests = st[2];
+        stats->bvh_node_tests = st[3];
+        stats->big_sphere_tests = use_bvh ? st[0] * (uint64_t)d->nbig : st[0] * (uint64_t)d->nsph;
     }
     return 0;
 }

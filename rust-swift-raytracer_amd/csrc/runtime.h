@@ -8,6 +8,7 @@
 #include <memory>
 #include <string>
 
+#include "bvh.h"
 #include "scene.h"
 
 struct RtRenderOptions;
@@ -28,12 +29,15 @@ struct DeviceState {
     float4 *sph_hot = nullptr, *sph_cold = nullptr, *tri_hot = nullptr, *tri_geo = nullptr;
     float *mats = nullptr;
     uint32_t nsph = 0, nsph_padded = 0, ntri = 0;
+    float4 *bvh_nodes = nullptr, *bvh_prims = nullptr, *big_hot = nullptr;
+    uint32_t *bvh_miss = nullptr, *bvh_prim_id = nullptr, *big_id = nullptr;
+    uint32_t nnodes = 0, nbig = 0;
     float4 *samples = nullptr;       size_t samples_cap = 0;   // per-sample colour slab
     uint32_t *out = nullptr;         size_t out_cap = 0;       // RGBA8 tile (host path)
     uint32_t *replay = nullptr;      size_t replay_cap = 0;
     uint32_t *counter = nullptr;                                // job counter
     unsigned long long *stats = nullptr;                        // [rays, tri_in_range]
-    int blocks_per_cu = 0, num_cus = 0;
+    int blocks_per_cu = 0, blocks_per_cu_bvh = 0, num_cus = 0;
     size_t last_jobs = 0;                                       // jobs of the last launch
     ~DeviceState();
 };
@@ -41,6 +45,7 @@ struct DeviceState {
 struct WorldState {
     SceneModel scene;
     PackedScene packed;
+    SphereBVH bvh;
     std::map<int, std::unique_ptr<DeviceState>> devices;
 };
 

@@ -18,6 +18,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "lib", "libraytracer.so")
 
 RNG_COUNTER, RNG_REPLAY = 1, 2
+ACCEL_AUTO, ACCEL_BRUTE, ACCEL_BVH = 0, 1, 2
 DEFAULT_SEED = 2547549
 
 # Every symbol declared in include/raytracer.h and include/raytracer_amd.h.
@@ -50,14 +51,17 @@ class RenderOptions(C.Structure):
     _fields_ = [("samples_per_pixel", C.c_int32), ("max_ray_bounces", C.c_int32),
                 ("rng_mode", C.c_uint32), ("seed", C.c_uint32),
                 ("replay_states", C.POINTER(C.c_uint32)), ("row_block", C.c_uint32),
-                ("rank", C.c_uint32), ("nranks", C.c_uint32), ("device", C.c_int32)]
+                ("rank", C.c_uint32), ("nranks", C.c_uint32), ("device", C.c_int32),
+                ("accel", C.c_int32)]
 
 
 class RenderStats(C.Structure):
     _fields_ = [("samples", C.c_uint64), ("rays", C.c_uint64), ("sphere_tests", C.c_uint64),
                 ("tri_tests", C.c_uint64), ("tri_in_range", C.c_uint64),
                 ("trace_ms", C.c_double), ("resolve_ms", C.c_double),
-                ("trace_launches", C.c_uint32), ("waves", C.c_uint32)]
+                ("trace_launches", C.c_uint32), ("waves", C.c_uint32), ("accel", C.c_uint32),
+                ("bvh_sphere_tests", C.c_uint64), ("bvh_node_tests", C.c_uint64),
+                ("big_sphere_tests", C.c_uint64)]
 
     def as_dict(self):
         return {k: (float(getattr(self, k)) if t is C.c_double else int(getattr(self, k)))
@@ -140,11 +144,12 @@ def sample_seed(seed: int, job: int) -> int:
 
 
 def options(spp=16, depth=8, mode=RNG_COUNTER, seed=DEFAULT_SEED, replay=None, row_block=1,
-            rank=0, nranks=1, device=-1):
+            rank=0, nranks=1, device=-1, accel=ACCEL_AUTO):
     o = RenderOptions()
     lib().rt_default_options(C.byref(o))
     o.samples_per_pixel, o.max_ray_bounces, o.rng_mode, o.seed = spp, depth, mode, seed
     o.row_block, o.rank, o.nranks, o.device = row_block, rank, nranks, device
+    o.accel = accel
     keep = None
     if replay is not None:
         keep = np.ascontiguousarray(replay, dtype=np.uint32)
@@ -212,9 +217,9 @@ class World:
         return px
 
     def render(self, width, height, spp=16, depth=8, mode=RNG_COUNTER, seed=DEFAULT_SEED,
-               replay=None, row_block=1, rank=0, nranks=1, device=-1):
+               replay=None, row_block=1, rank=0, nranks=1, device=-1, accel=ACCEL_AUTO):
         """rt_render_ex -> (rgba uint8[tile_rows, width, 4], stats dict)."""
-        o, keep = options(spp, depth, mode, seed, replay, row_block, rank, nranks, device)
+        o, keep = options(spp, depth, mode, seed, replay, row_block, rank, nranks, device, accel)
         rows = tile_rows(height, row_block, rank, nranks) if nranks > 1 else height
         px = np.zeros((rows, width, 4), np.uint8)
         fb = CFramebuffer(width, height, px.ctypes.data_as(C.POINTER(ColorU8)))
@@ -236,9 +241,9 @@ class World:
 
     def render_device(self, width, height, out_ptr: int, stream_ptr: int = 0, spp=16, depth=8,
                       mode=RNG_COUNTER, seed=DEFAULT_SEED, row_block=1, rank=0, nranks=1,
-                      device=-1):
+                      device=-1, accel=ACCEL_AUTO):
         """rt_render_device into a device buffer (e.g. a torch uint8 tensor)."""
-        o, _ = options(spp, depth, mode, seed, None, row_block, rank, nranks, device)
+        o, _ = options(spp, depth, mode, seed, None, row_block, rank, nranks, device, accel)
         st = RenderStats()
         rc = lib().rt_render_device(self._h, width, height, C.byref(o), C.c_void_p(out_ptr),
                                     C.c_void_p(stream_ptr or None), C.byref(st))

@@ -220,3 +220,72 @@ def test_full_size_c2_properties():
         ref.render(W, H, spp, depth, mode=O.RNG_COUNTER, row_begin=r, row_step=H, nthreads=8,
                    out=img)
         assert_bits_equal(a[H - 1 - r], img[H - 1 - r], f"row {r}")
+
+
+# ---------------------------------------------------------------- exact BVH
+def _random_scene(seed, n, spread, radius, offset=(0.0, 0.0, 0.0), dup=0, big=True,
+                  cam=(0.0, 0.0, 0.0)):
+    rng = np.random.default_rng(seed)
+    kinds = ["Diffuse color 0.7 0.5 0.3", "Metal color 0.9 0.8 0.7 fuzz 0.05",
+             "Dielectric ir 1.5", "Metal color 0.6 0.6 0.9 fuzz 0.0"]
+    lines = [f"camera origin {cam[0]:.6f} {cam[1]:.6f} {cam[2]:.6f} aspect 1.5;"]
+    lines += [f"material K{i} : {k};" for i, k in enumerate(kinds)]
+    sph = []
+    if big:
+        sph.append((offset[0], offset[1] - 1000.0, offset[2], 999.0, 0))
+    for _ in range(n):
+        c = rng.uniform(-spread, spread, 3) + np.array(offset) + np.array([0, 0, -spread - 2])
+        r = radius * rng.uniform(0.3, 1.0)
+        sph.append((c[0], c[1], c[2], r, int(rng.integers(0, 4))))
+    sph += sph[1:1 + dup]  # exact duplicates: equal t, the lower index must win
+    for (x, y, z, r, k) in sph:
+        lines.append(f"sphere center {x:.6f} {y:.6f} {z:.6f} radius {r:.6f} material K{k};")
+    return "\n".join(lines) + "\n"
+
+
+def _both_modes(src, w, h, spp, depth=8):
+    world = R.World(src)
+    a, sa = world.render(w, h, spp, depth, accel=R.ACCEL_BRUTE)
+    sma = world.read_samples(w * h * spp)
+    b, sb = world.render(w, h, spp, depth, accel=R.ACCEL_BVH)
+    smb = world.read_samples(w * h * spp)
+    return a, sa, sma, b, sb, smb
+
+
+@pytest.mark.parametrize("case", [
+    dict(seed=1, n=400, spread=6.0, radius=0.3),
+    dict(seed=2, n=300, spread=3.0, radius=0.6, dup=40),
+    dict(seed=3, n=500, spread=20.0, radius=0.05),
+    dict(seed=4, n=200, spread=5.0, radius=0.4, offset=(3000.0, -2000.0, 1500.0),
+         cam=(3000.0, -2000.0, 1500.0)),
+    dict(seed=5, n=250, spread=2.0, radius=0.5, big=False, cam=(0.0, 0.0, -4.0)),
+])
+def test_bvh_equals_brute_force(case):
+    src = _random_scene(**case)
+    a, sa, sma, b, sb, smb = _both_modes(src, 96, 64, 8)
+    assert sb["accel"] == R.ACCEL_BVH and sa["accel"] == R.ACCEL_BRUTE
+    assert_bits_equal(b, a, "frame")
+    assert_bits_equal(smb[:, :3], sma[:, :3], "samples")
+    assert sa["rays"] == sb["rays"]
+    assert sb["bvh_sphere_tests"] + sb["big_sphere_tests"] < sa["sphere_tests"]
+
+
+def test_bvh_matches_oracle_rtow():
+    src = S.rtow()
+    img, st, _, smp = O.Scene(src).render(64, 36, 4, 8, mode=O.RNG_COUNTER, nthreads=8,
+                                          record_samples=True)
+    world = R.World(src)
+    out, gst = world.render(64, 36, 4, 8, accel=R.ACCEL_BVH)
+    assert gst["accel"] == R.ACCEL_BVH
+    assert_bits_equal(out, img, "frame")
+    assert_bits_equal(world.read_samples(64 * 36 * 4)[:, :3],
+                      oracle_samples_to_gpu_order(smp, 64, 36, 4)[:, :3], "samples")
+    assert gst["rays"] == st["rays"]
+
+
+def test_bvh_full_size_c2_equals_brute_force():
+    """Every pixel and every sample colour of a 1920x1080x16 RTOW frame."""
+    a, sa, sma, b, sb, smb = _both_modes(S.rtow(), 1920, 1080, 16)
+    assert_bits_equal(b, a, "frame")
+    assert np.array_equal(smb[:, :3].view(np.uint32), sma[:, :3].view(np.uint32))
+    assert sa["rays"] == sb["rays"]
