@@ -40,11 +40,24 @@ HBM_PEAK_GBS = 8000.0
 ROW_BLOCK = 8  # multi-GPU: row-cyclic blocks of 8 image rows
 
 
+NODE_TEST_FLOPS = 26  # slab test: 6 sub, 6 mul, 10 min/max, 4 slack mul/compare
+
+
 def algorithmic_flops(st):
     """17*sphere_tests + 14*tri_tests + 60*tri_in_range
-    + 40*rays + 20*samples (no FMA: every add/mul/div/sqrt/compare is 1)."""
+    + 40*rays + 20*samples (no FMA: every add/mul/div/sqrt/compare is 1),
+    with sphere_tests = rays * spheres (the reference's brute force)."""
     return (17 * st["sphere_tests"] + 14 * st["tri_tests"] + 60 * st["tri_in_range"]
             + 40 * st["rays"] + 20 * st["samples"])
+
+
+def executed_flops(st):
+    """The same price list applied to the work the kernel actually executed:
+    sphere tests done (BVH leaves + spheres kept out of the tree, or all of
+    them in brute force) plus NODE_TEST_FLOPS per BVH box test."""
+    sph = st["bvh_sphere_tests"] + st["big_sphere_tests"]
+    return (17 * sph + NODE_TEST_FLOPS * st["bvh_node_tests"] + 14 * st["tri_tests"]
+            + 60 * st["tri_in_range"] + 40 * st["rays"] + 20 * st["samples"])
 
 
 def cpu_baseline(src, W, H, spp, depth, budget_s):
@@ -79,6 +92,7 @@ def main():
     ap.add_argument("--config", default="c2", choices=sorted(S.CONFIGS))
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--accel", default="auto", choices=["auto", "brute", "bvh"])
     args = ap.parse_args()
 
     world_size = int(os.environ.get("WORLD_SIZE", "1"))
@@ -89,6 +103,7 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
 
     make_scene, W, H, spp, depth = S.CONFIGS[args.config]
+    accel = {"auto": R.ACCEL_AUTO, "brute": R.ACCEL_BRUTE, "bvh": R.ACCEL_BVH}[args.accel]
     src = make_scene()
     world = R.World(src)
     nr = world_size
@@ -101,7 +116,8 @@ def main():
 
     def step():
         st = world.render_device(W, H, tile.data_ptr(), stream.cuda_stream, spp=spp, depth=depth,
-                                 row_block=ROW_BLOCK, rank=rank, nranks=nr, device=local_rank)
+                                 row_block=ROW_BLOCK, rank=rank, nranks=nr, device=local_rank,
+                                 accel=accel)
         if nr > 1:
             tiles.gather(tile, gathered)  # RCCL all-gather over xGMI
         return st
@@ -131,8 +147,9 @@ def main():
 
     st0 = stats[-1]
     launches = max(1, st0["trace_launches"])
-    flops_per_launch = algorithmic_flops(st0) / launches
+    flops_per_launch = executed_flops(st0) / launches
     achieved_tflops = flops_per_launch / (trace_ms * 1e-3) / 1e12
+    alg_tflops = algorithmic_flops(st0) / launches / (trace_ms * 1e-3) / 1e12
     out_bytes = rows * W * 4
     traffic = None
     tfile = os.path.join(ROOT, "profiles", "hbm_traffic.json")
@@ -163,10 +180,15 @@ def main():
                      "peak": FP32_VECTOR_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": achieved_tflops / FP32_VECTOR_PEAK_TFLOPS, "traffic": traffic,
                      "kernel": "trace_kernel", "avg_launch_ms": trace_ms,
-                     "flops_per_launch": flops_per_launch,
+                     "flops_per_launch": flops_per_launch, "flops": "executed work",
+                     "brute_force_equivalent_tflops": alg_tflops,
                      "algorithmic_hbm_gbs": out_bytes / (trace_ms * 1e-3) / 1e9,
                      "hbm_peak_gbs": HBM_PEAK_GBS},
         "rays_per_frame": st0["rays"],
+        "accel": {1: "brute", 2: "bvh"}.get(st0["accel"], "?"),
+        "per_ray": {"sphere_tests": (st0["bvh_sphere_tests"] + st0["big_sphere_tests"]) / st0["rays"],
+                    "node_tests": st0["bvh_node_tests"] / st0["rays"],
+                    "brute_force_sphere_tests": st0["sphere_tests"] / st0["rays"]},
     }
     if nr == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(src, W, H, spp, depth, args.cpu_seconds)
