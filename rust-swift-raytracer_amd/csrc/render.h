@@ -5,6 +5,8 @@
 
 #include <cstdint>
 
+#include "fastdiv.h"
+
 namespace rtamd {
 
 enum : uint32_t { kRngCounter = 1, kRngReplay = 2 };
@@ -35,11 +37,17 @@ struct TraceParams {
     // exact-pruning BVH (bvh.h); nnodes == 0 selects the brute-force kernel
     const float4 *bvh_nodes;  // 2 per node
     const uint32_t *bvh_miss; // 8 per node (one DFS successor per ray octant)
+    const uint16_t *bvh_miss16;  // same as u16 (0xFFFF = end), for the LDS copy
     const float4 *bvh_prims;  // (cx, cy, cz, r*r) in BVH order
     const uint32_t *bvh_prim_id;
     const float4 *big_hot;    // spheres kept out of the tree (tested first)
     const uint32_t *big_id;
-    uint32_t nnodes, nbig;
+    uint32_t nnodes, nbig, nprims;
+    uint32_t use_lds;         // stage the tree in LDS (trace_lds_bytes per workgroup)
+    uint32_t ablate;          // timing-only diagnostics (RT_AMD_ABLATE): 1 = skip the tree walk
+    const float4 *sph_shade;  // 2 per sphere: (centre, r) (colour, fuzz|ir)
+    const uint32_t *sph_kind; // material kind per sphere
+    FastDiv div_spp, div_width, div_rowblock;  // job -> pixel mapping
     float bvh_c[3], bvh_r, bvh_rmax, bvh_mag;
 };
 
@@ -48,6 +56,8 @@ hipError_t launch_trace(const TraceParams &p, uint32_t blocks, hipStream_t strea
 hipError_t launch_resolve_ex(const float4 *samples, uint32_t *out, uint32_t npix, uint32_t spp,
                              float inv_spp, uint32_t width, uint32_t slab_row0,
                              hipStream_t stream);
-hipError_t trace_occupancy(int *blocks_per_cu, bool bvh);
+// variant: 0 brute force, 1 BVH from global memory, 2 BVH staged in LDS
+hipError_t trace_occupancy(int *blocks_per_cu, int variant, size_t lds_bytes);
+size_t trace_lds_bytes(const TraceParams &p);
 
 }  // namespace rtamd

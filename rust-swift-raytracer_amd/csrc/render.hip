@@ -95,6 +95,8 @@ __device__ __forceinline__ float4 uniform_load(const float4 *base, uint32_t i) {
 #endif
 }
 
+__device__ __forceinline__ uint32_t fdiv(uint32_t n, const FastDiv &f) { return fastdiv_apply(n, f); }
+
 constexpr uint32_t kWave = 64;
 constexpr uint32_t kNodeEndDev = 0xFFFFFFFFu;  // bvh.h kNodeEnd
 constexpr uint32_t kLeafBitDev = 0x80000000u;  // bvh.h kLeafBit
@@ -168,21 +170,34 @@ __device__ __forceinline__ float upper_rel(float x) { return x * (x > 0.0f ? 1.0
 
 constexpr float kErrK = 3.0e-3f;  // >= 2.7x the derived sqrt(30u) = 1.12e-3
 
+// Where the traversal reads the tree from: global memory (any size) or the
+// workgroup's LDS copy (staged once per persistent workgroup).
+struct BvhView {
+    const float4 *nodes;     // 2 per node
+    const uint32_t *miss32;  // global: 8 x u32 per node
+    const uint16_t *miss16;  // LDS: 8 x u16 per node
+    const float4 *prims;
+    const uint32_t *ids;
+    const float4 *shade;     // per-sphere shading records (2 x float4)
+    const uint32_t *kinds;
+};
+
 // Spheres through the exact-pruning BVH (bvh.h).  Big spheres first (brute
 // force, wave-uniform), then a stackless octant-ordered traversal: every
 // node box is inflated per ray by e = K*(min(A, best_t + R)*(1+3K) + R) + e_abs,
 // which bounds how far a computed candidate's point can lie outside its
 // sphere; a node is skipped only when the inflated box is certainly missed
 // or certainly starts beyond best_t.
-__device__ __forceinline__ void spheres_bvh(const TraceParams &p, F3 org, F3 dir, float &best_t,
-                                            int &best_i, uint32_t &sph_tests,
+template <bool kLds>
+__device__ __forceinline__ void spheres_bvh(const TraceParams &p, const BvhView &v, F3 org, F3 dir,
+                                            float &best_t, int &best_i, uint32_t &sph_tests,
                                             uint32_t &node_tests) {
     for (uint32_t k = 0; k < p.nbig; ++k) {
         const float4 S = uniform_load(p.big_hot, k);
         const int idx = (int)p.big_id[k];
         sphere_candidate(S, org, dir, idx, best_t, best_i);
     }
-    if (p.nnodes == 0) return;
+    if (p.ablate & 1u) return;  // timing-only diagnostic build path: results are wrong
     const float ix = 1.0f / dir.x, iy = 1.0f / dir.y, iz = 1.0f / dir.z;
     const uint32_t oct = (ix < 0.0f ? 1u : 0u) | (iy < 0.0f ? 2u : 0u) | (iz < 0.0f ? 4u : 0u);
     const float ax = org.x - p.bvh_c[0], ay = org.y - p.bvh_c[1], az = org.z - p.bvh_c[2];
@@ -195,11 +210,13 @@ __device__ __forceinline__ void spheres_bvh(const TraceParams &p, F3 org, F3 dir
     float e = inflation(best_t);
     F3 lo = f3(org.x + e, org.y + e, org.z + e);  // (bmin - e) - o == bmin - (o + e)
     F3 hi = f3(org.x - e, org.y - e, org.z - e);
+    const uint32_t kEnd = kLds ? 0xFFFFu : kNodeEndDev;
     uint32_t node = 0;
-    while (node != kNodeEndDev) {
+    while (node != kEnd) {
         ++node_tests;
-        const float4 B0 = p.bvh_nodes[2 * node];
-        const float4 B1 = p.bvh_nodes[2 * node + 1];
+        const float4 B0 = v.nodes[2 * node];
+        const float4 B1 = v.nodes[2 * node + 1];
+        const uint32_t miss = kLds ? (uint32_t)v.miss16[8 * node + oct] : v.miss32[8 * node + oct];
         const float t0x = (B0.x - lo.x) * ix, t1x = (B1.x - hi.x) * ix;
         const float t0y = (B0.y - lo.y) * iy, t1y = (B1.y - hi.y) * iy;
         const float t0z = (B0.z - lo.z) * iz, t1z = (B1.z - hi.z) * iz;
@@ -209,21 +226,20 @@ __device__ __forceinline__ void spheres_bvh(const TraceParams &p, F3 org, F3 dir
                           lower_rel(tn) > upper_rel(best_t);
         const uint32_t a = __float_as_uint(B0.w);
         if (skip) {
-            node = p.bvh_miss[8 * node + oct];
+            node = miss;
         } else if (a & kLeafBitDev) {
             const uint32_t first = a & ~kLeafBitDev, count = __float_as_uint(B1.w);
             bool changed = false;
             for (uint32_t j = first; j < first + count; ++j) {
                 ++sph_tests;
-                changed |= sphere_candidate(p.bvh_prims[j], org, dir, (int)p.bvh_prim_id[j], best_t,
-                                            best_i);
+                changed |= sphere_candidate(v.prims[j], org, dir, (int)v.ids[j], best_t, best_i);
             }
             if (changed) {
                 e = inflation(best_t);
                 lo = f3(org.x + e, org.y + e, org.z + e);
                 hi = f3(org.x - e, org.y - e, org.z - e);
             }
-            node = p.bvh_miss[8 * node + oct];
+            node = miss;
         } else {
             node = a + ((oct >> __float_as_uint(B1.w)) & 1u);  // near child first
         }
@@ -231,9 +247,41 @@ __device__ __forceinline__ void spheres_bvh(const TraceParams &p, F3 org, F3 dir
 }
 
 // ------------------------------------------------------------ trace kernel
-template <bool kBvh>
-__global__ __launch_bounds__(256) void trace_kernel(TraceParams p) {
+// kBvh: sphere search through the exact BVH (else brute force).  kLds: the
+// tree is copied into the workgroup's LDS once (persistent grid), so every
+// traversal step is a ds_read instead of an L2 round trip.
+template <bool kBvh, bool kLds>
+__global__ __launch_bounds__(kLds ? 512 : 256) void trace_kernel(TraceParams p) {
     const uint32_t lane = __lane_id();
+    extern __shared__ float4 lds[];
+    BvhView view;
+    if (kLds) {
+        // layout: nodes (2 x float4 / node) | prims (float4) | shade (2 x float4 /
+        // sphere) | ids (u32) | kinds (u32) | miss (8 x u16 / node)
+        float4 *n4 = lds;
+        float4 *p4 = n4 + 2 * p.nnodes;
+        float4 *s4 = p4 + p.nprims;
+        uint32_t *id = reinterpret_cast<uint32_t *>(s4 + 2 * p.nsph_padded);
+        uint32_t *kd = id + p.nprims;
+        uint32_t *m32 = kd + p.nsph_padded;  // miss16 viewed as u32 words (4 per node)
+        for (uint32_t i = threadIdx.x; i < 2 * p.nnodes; i += blockDim.x) n4[i] = p.bvh_nodes[i];
+        for (uint32_t i = threadIdx.x; i < p.nprims; i += blockDim.x) {
+            p4[i] = p.bvh_prims[i];
+            id[i] = p.bvh_prim_id[i];
+        }
+        for (uint32_t i = threadIdx.x; i < p.nsph_padded; i += blockDim.x) {
+            s4[2 * i] = p.sph_shade[2 * i];
+            s4[2 * i + 1] = p.sph_shade[2 * i + 1];
+            kd[i] = p.sph_kind[i];
+        }
+        const uint32_t *g16 = reinterpret_cast<const uint32_t *>(p.bvh_miss16);
+        for (uint32_t i = threadIdx.x; i < 4 * p.nnodes; i += blockDim.x) m32[i] = g16[i];
+        __syncthreads();
+        view = BvhView{n4, nullptr, reinterpret_cast<const uint16_t *>(m32), p4, id, s4, kd};
+    } else {
+        view = BvhView{p.bvh_nodes, p.bvh_miss, nullptr, p.bvh_prims, p.bvh_prim_id,
+                       p.sph_shade, p.sph_kind};
+    }
     const float tmin = 0.001f;                 // common.rs:242, 250
 
     F3 org = f3(0, 0, 0), dir = f3(0, 0, 0);
@@ -266,14 +314,14 @@ __global__ __launch_bounds__(256) void trace_kernel(TraceParams p) {
             if (!active && rank < avail) {
                 const uint32_t job = pool_next + rank;
                 // job -> (tile row, column, sample) -> reference (row, col)
-                const uint32_t lp = job / p.spp;
+                const uint32_t lp = fdiv(job, p.div_spp);
                 const uint32_t s = job - lp * p.spp;
                 slot = s * p.npix + lp;  // sample-major slab: resolve reads coalesce
-                const uint32_t q = lp / p.width;
+                const uint32_t q = fdiv(lp, p.div_width);
                 const uint32_t col = lp - q * p.width;
                 const uint32_t lr = p.slab_row0 + q;
-                const uint32_t ir = ((lr / p.row_block) * p.nranks + p.rank) * p.row_block +
-                                    lr % p.row_block;
+                const uint32_t blk = fdiv(lr, p.div_rowblock);
+                const uint32_t ir = (blk * p.nranks + p.rank) * p.row_block + (lr - blk * p.row_block);
                 const uint32_t row = p.height - 1u - ir;
                 const uint64_t gjob = ((uint64_t)row * p.width + col) * p.spp + s;
                 rng = (p.mode == kRngReplay) ? p.replay[gjob] : counter_seed(p.seed, gjob);
@@ -308,7 +356,7 @@ __global__ __launch_bounds__(256) void trace_kernel(TraceParams p) {
             float best_t = __builtin_inff();
             int best_i = -1;
             if (kBvh) {
-                spheres_bvh(p, org, dir, best_t, best_i, sph_tests, node_tests);
+                spheres_bvh<kLds>(p, view, org, dir, best_t, best_i, sph_tests, node_tests);
             } else {
                 spheres_brute(p, org, dir, best_t, best_i);
             }
@@ -343,23 +391,25 @@ __global__ __launch_bounds__(256) void trace_kernel(TraceParams p) {
                 done = true;
             } else {
                 F3 pos, nrm;
-                uint32_t mid;
+                uint32_t kind;
+                float cr, cg, cb, param;
                 if (tri_i >= 0) {  // a triangle wins a tie against a sphere
                     pos = org + scale(dir, tri_t);
                     const float4 *g = p.tri_geo + 4u * (uint32_t)tri_i;
                     const float4 A = g[0], Nn = g[3];
                     nrm = f3(Nn.x, Nn.y, Nn.z);
-                    mid = __float_as_uint(A.w);
+                    const float *m = p.mats + 8u * __float_as_uint(A.w);
+                    kind = __float_as_uint(m[0]);
+                    cr = m[1]; cg = m[2]; cb = m[3]; param = m[4];
                 } else {
-                    const float4 S = p.sph_hot[best_i];
-                    const float4 Sc = p.sph_cold[best_i];
+                    // one round trip: centre/radius, colour/param and kind together
+                    const float4 S = view.shade[2 * best_i];
+                    const float4 M = view.shade[2 * best_i + 1];
+                    kind = view.kinds[best_i];
                     pos = org + scale(dir, best_t);
-                    nrm = unit(divide(pos - f3(S.x, S.y, S.z), Sc.x));  // common.rs:95
-                    mid = __float_as_uint(Sc.y);
+                    nrm = unit(divide(pos - f3(S.x, S.y, S.z), S.w));  // common.rs:95
+                    cr = M.x; cg = M.y; cb = M.z; param = M.w;
                 }
-                const float *m = p.mats + 8u * mid;
-                const uint32_t kind = __float_as_uint(m[0]);
-                float cr = m[1], cg = m[2], cb = m[3];
                 bool next = true;
                 F3 ndir;
                 if (kind == kMatDiffuse) {  // materials.rs:42-52
@@ -369,13 +419,13 @@ __global__ __launch_bounds__(256) void trace_kernel(TraceParams p) {
                     ndir = nz ? nrm : unit(sc);
                 } else if (kind == kMatMetal) {  // materials.rs:54-63
                     const F3 refl = dir - scale(nrm, 2.0f * dot(dir, nrm));
-                    const F3 d2 = refl + scale(draw_unit(rng), m[4]);
+                    const F3 d2 = refl + scale(draw_unit(rng), param);
                     next = dot(d2, nrm) >= 0.0f;
                     ndir = unit(d2);
                 } else if (kind == kMatDielectric) {  // materials.rs:65-97
                     F3 n2 = nrm;
-                    float eta = m[4];
-                    if (dot(dir, nrm) >= 0.0f) { n2 = -nrm; eta = 1.0f / m[4]; }
+                    float eta = param;
+                    if (dot(dir, nrm) >= 0.0f) { n2 = -nrm; eta = 1.0f / param; }
                     const float cos_t = dot(-dir, n2);  // maths.rs:31-36
                     const F3 perp = scale(dir + scale(n2, cos_t), eta);
                     const F3 par = scale(n2, -__builtin_sqrtf(fabsf(1.0f - dot(perp, perp))));
@@ -446,11 +496,18 @@ __global__ __launch_bounds__(256) void resolve_kernel(const float4 *__restrict__
 
 }  // namespace
 
+size_t trace_lds_bytes(const TraceParams &p) {
+    return (size_t)p.nnodes * 48 + (size_t)p.nprims * 20 + (size_t)p.nsph_padded * 36;
+}
+
 hipError_t launch_trace(const TraceParams &p, uint32_t blocks, hipStream_t stream) {
-    if (p.nnodes)
-        hipLaunchKernelGGL(trace_kernel<true>, dim3(blocks), dim3(256), 0, stream, p);
+    if (p.nnodes && p.use_lds)
+        hipLaunchKernelGGL((trace_kernel<true, true>), dim3(blocks), dim3(512), trace_lds_bytes(p),
+                           stream, p);
+    else if (p.nnodes)
+        hipLaunchKernelGGL((trace_kernel<true, false>), dim3(blocks), dim3(256), 0, stream, p);
     else
-        hipLaunchKernelGGL(trace_kernel<false>, dim3(blocks), dim3(256), 0, stream, p);
+        hipLaunchKernelGGL((trace_kernel<false, false>), dim3(blocks), dim3(256), 0, stream, p);
     return hipGetLastError();
 }
 
@@ -463,9 +520,14 @@ hipError_t launch_resolve_ex(const float4 *samples, uint32_t *out, uint32_t npix
     return hipGetLastError();
 }
 
-hipError_t trace_occupancy(int *blocks_per_cu, bool bvh) {
-    if (bvh) return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, trace_kernel<true>, 256, 0);
-    return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, trace_kernel<false>, 256, 0);
+hipError_t trace_occupancy(int *blocks_per_cu, int variant, size_t lds_bytes) {
+    if (variant == 2)
+        return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, trace_kernel<true, true>,
+                                                            512, lds_bytes);
+    if (variant == 1)
+        return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, trace_kernel<true, false>,
+                                                            256, 0);
+    return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, trace_kernel<false, false>, 256, 0);
 }
 
 }  // namespace rtamd

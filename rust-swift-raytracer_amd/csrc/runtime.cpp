@@ -44,7 +44,8 @@ DeviceState::~DeviceState() {
     if (device < 0) return;
     if (hipSetDevice(device) != hipSuccess) return;
     void *bufs[] = {sph_hot, sph_cold, tri_hot, tri_geo, mats, samples, out, replay, counter, stats,
-                    bvh_nodes, bvh_prims, big_hot, bvh_miss, bvh_prim_id, big_id};
+                    bvh_nodes, bvh_prims, big_hot, bvh_miss, bvh_prim_id, big_id, bvh_miss16,
+                    sph_shade, sph_kind};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
     for (hipEvent_t e : ev)
@@ -89,12 +90,8 @@ static int device_for(WorldState &w, int want, DeviceState *&out) {
         hipDeviceProp_t prop;
         HIP_TRY(hipGetDeviceProperties(&prop, dev));
         d->num_cus = prop.multiProcessorCount;
-        HIP_TRY(trace_occupancy(&d->blocks_per_cu, false));
-        HIP_TRY(trace_occupancy(&d->blocks_per_cu_bvh, true));
-        const uint64_t bpc = env_u64("RT_AMD_BLOCKS_PER_CU", 0);
-        if (bpc) d->blocks_per_cu = d->blocks_per_cu_bvh = (int)bpc;
-        if (d->blocks_per_cu < 1) d->blocks_per_cu = 1;
-        if (d->blocks_per_cu_bvh < 1) d->blocks_per_cu_bvh = 1;
+        HIP_TRY(trace_occupancy(&d->blocks_per_cu, 0, 0));
+        HIP_TRY(trace_occupancy(&d->blocks_per_cu_bvh, 1, 0));
         // scene upload (once per device)
         const PackedScene &p = w.packed;
         auto up = [&](void **dst, const std::vector<float> &src) -> hipError_t {
@@ -107,6 +104,9 @@ static int device_for(WorldState &w, int want, DeviceState *&out) {
         HIP_TRY(up((void **)&d->tri_hot, p.tri_hot));
         HIP_TRY(up((void **)&d->tri_geo, p.tri_geo));
         HIP_TRY(up((void **)&d->mats, p.mats));
+        HIP_TRY(up((void **)&d->sph_shade, p.sph_shade));
+        HIP_TRY(hipMalloc((void **)&d->sph_kind, p.sph_kind.size() * 4));
+        HIP_TRY(hipMemcpy(d->sph_kind, p.sph_kind.data(), p.sph_kind.size() * 4, hipMemcpyHostToDevice));
         d->nsph = p.nsph;
         d->nsph_padded = p.nsph_padded;
         d->ntri = p.ntri;
@@ -129,7 +129,24 @@ static int device_for(WorldState &w, int want, DeviceState *&out) {
             HIP_TRY(upu((void **)&d->big_id, bv.big));
             d->nnodes = (uint32_t)(bv.nodes.size() / 8);
             d->nbig = (uint32_t)bv.big.size();
+            d->nprims = (uint32_t)bv.prim_id.size();
+            // LDS copy of the tree: 48 B per node + 20 B per sphere, u16 links
+            const size_t lds = (size_t)d->nnodes * 48 + (size_t)d->nprims * 20 +
+                               (size_t)p.nsph_padded * 36;
+            if (d->nnodes < 0xFFFF && lds <= env_u64("RT_AMD_LDS_MAX", 64 * 1024)) {
+                std::vector<uint16_t> m16(bv.miss.size());
+                for (size_t i = 0; i < m16.size(); ++i)
+                    m16[i] = bv.miss[i] == kNodeEnd ? (uint16_t)0xFFFF : (uint16_t)bv.miss[i];
+                HIP_TRY(hipMalloc((void **)&d->bvh_miss16, m16.size() * 2));
+                HIP_TRY(hipMemcpy(d->bvh_miss16, m16.data(), m16.size() * 2, hipMemcpyHostToDevice));
+                HIP_TRY(trace_occupancy(&d->blocks_per_cu_lds, 2, lds));
+                if (d->blocks_per_cu_lds > 0) d->lds_bytes = lds;
+            }
         }
+        const uint64_t bpc = env_u64("RT_AMD_BLOCKS_PER_CU", 0);
+        if (bpc) d->blocks_per_cu = d->blocks_per_cu_bvh = d->blocks_per_cu_lds = (int)bpc;
+        if (d->blocks_per_cu < 1) d->blocks_per_cu = 1;
+        if (d->blocks_per_cu_bvh < 1) d->blocks_per_cu_bvh = 1;
         HIP_TRY(hipMalloc((void **)&d->counter, 64));
         HIP_TRY(hipMalloc((void **)&d->stats, 64));
         slot = std::move(d);
@@ -202,6 +219,12 @@ int render_frame(WorldState &w, const CameraModel &cam, size_t width, size_t hei
     p.width = (uint32_t)width; p.height = (uint32_t)height; p.spp = spp;
     p.depth = o.max_ray_bounces;
     p.mode = o.rng_mode; p.seed = o.seed;
+    p.ablate = (uint32_t)env_u64("RT_AMD_ABLATE", 0);
+    p.sph_shade = d->sph_shade;
+    p.sph_kind = d->sph_kind;
+    p.div_spp = make_fastdiv(spp);
+    p.div_width = make_fastdiv((uint32_t)width);
+    p.div_rowblock = make_fastdiv(B);
     p.row_block = B; p.rank = o.rank; p.nranks = nranks;
     const bool use_bvh = d->nnodes > 0 && o.accel != RT_ACCEL_BRUTE;
     if (use_bvh) {
@@ -209,14 +232,17 @@ int render_frame(WorldState &w, const CameraModel &cam, size_t width, size_t hei
         p.bvh_nodes = d->bvh_nodes; p.bvh_miss = d->bvh_miss;
         p.bvh_prims = d->bvh_prims; p.bvh_prim_id = d->bvh_prim_id;
         p.big_hot = d->big_hot; p.big_id = d->big_id;
-        p.nnodes = d->nnodes; p.nbig = d->nbig;
+        p.nnodes = d->nnodes; p.nbig = d->nbig; p.nprims = d->nprims;
+        p.bvh_miss16 = d->bvh_miss16;
+        p.use_lds = d->lds_bytes > 0 && env_u64("RT_AMD_LDS", 1) != 0;
         for (int k = 0; k < 3; ++k) p.bvh_c[k] = bv.centre[k];
         p.bvh_r = bv.radius; p.bvh_rmax = bv.rmax; p.bvh_mag = bv.mag;
     }
     const float inv_spp = 1.0f / (float)o.samples_per_pixel;  // 1.0 / spp as f32 (common.rs:345)
 
-    const uint64_t full_blocks =
-        (uint64_t)(use_bvh ? d->blocks_per_cu_bvh : d->blocks_per_cu) * (uint64_t)d->num_cus;
+    const int bpc = !use_bvh ? d->blocks_per_cu : p.use_lds ? d->blocks_per_cu_lds : d->blocks_per_cu_bvh;
+    const uint64_t waves_per_block = (use_bvh && p.use_lds) ? 8 : 4;
+    const uint64_t full_blocks = (uint64_t)bpc * (uint64_t)d->num_cus;
     double trace_ms = 0.0, resolve_ms = 0.0;
     uint32_t launches = 0, waves = 0;
     for (size_t r0 = 0; r0 < T; r0 += rows_per_slab) {
@@ -227,9 +253,10 @@ int render_frame(WorldState &w, const CameraModel &cam, size_t width, size_t hei
         p.npix = (uint32_t)(rows * width);
         HIP_TRY(hipEventRecord(d->ev[0], s));
         if (njobs) {
-            uint64_t blocks = std::min<uint64_t>(full_blocks, (njobs + 1023) / 1024);
+            const uint64_t jobs_per_block = waves_per_block * 256;
+            uint64_t blocks = std::min<uint64_t>(full_blocks, (njobs + jobs_per_block - 1) / jobs_per_block);
             blocks = std::max<uint64_t>(blocks, 1);
-            const uint64_t nwaves = blocks * 4;
+            const uint64_t nwaves = blocks * waves_per_block;
             uint64_t chunk = env_u64("RT_AMD_CHUNK", 0);
             if (!chunk) chunk = std::min<uint64_t>(256, std::max<uint64_t>(64, njobs / (nwaves * 16) / 64 * 64));
             p.chunk = (uint32_t)chunk;

@@ -28,16 +28,20 @@ struct DeviceState {
     hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
     float4 *sph_hot = nullptr, *sph_cold = nullptr, *tri_hot = nullptr, *tri_geo = nullptr;
     float *mats = nullptr;
+    float4 *sph_shade = nullptr;
+    uint32_t *sph_kind = nullptr;
     uint32_t nsph = 0, nsph_padded = 0, ntri = 0;
     float4 *bvh_nodes = nullptr, *bvh_prims = nullptr, *big_hot = nullptr;
     uint32_t *bvh_miss = nullptr, *bvh_prim_id = nullptr, *big_id = nullptr;
-    uint32_t nnodes = 0, nbig = 0;
+    uint16_t *bvh_miss16 = nullptr;
+    uint32_t nnodes = 0, nbig = 0, nprims = 0;
+    size_t lds_bytes = 0;                                       // 0: tree not LDS-stageable
     float4 *samples = nullptr;       size_t samples_cap = 0;   // per-sample colour slab
     uint32_t *out = nullptr;         size_t out_cap = 0;       // RGBA8 tile (host path)
     uint32_t *replay = nullptr;      size_t replay_cap = 0;
     uint32_t *counter = nullptr;                                // job counter
     unsigned long long *stats = nullptr;                        // [rays, tri_in_range]
-    int blocks_per_cu = 0, blocks_per_cu_bvh = 0, num_cus = 0;
+    int blocks_per_cu = 0, blocks_per_cu_bvh = 0, blocks_per_cu_lds = 0, num_cus = 0;
     size_t last_jobs = 0;                                       // jobs of the last launch
     ~DeviceState();
 };

@@ -306,6 +306,16 @@ PackedScene pack_scene(const SceneModel &s, uint32_t sphere_pad, uint32_t tri_pa
         g[8] = t.v2.x; g[9] = t.v2.y; g[10] = t.v2.z;
         g[12] = t.normal.x; g[13] = t.normal.y; g[14] = t.normal.z;
     }
+    p.sph_shade.assign((size_t)p.nsph_padded * 8, 0.0f);
+    p.sph_kind.assign(p.nsph_padded, 0u);
+    for (uint32_t i = 0; i < p.nsph; ++i) {
+        const Sphere &q = s.spheres[i];
+        const Material &m = s.materials[q.material];
+        float *o = &p.sph_shade[(size_t)i * 8];
+        o[0] = q.center.x; o[1] = q.center.y; o[2] = q.center.z; o[3] = q.radius;
+        o[4] = m.r; o[5] = m.g; o[6] = m.b; o[7] = m.param;
+        p.sph_kind[i] = m.kind;
+    }
     p.mats.assign(s.materials.size() ? s.materials.size() * 8 : 8, 0.0f);
     for (size_t i = 0; i < s.materials.size(); ++i) {
         const Material &m = s.materials[i];

@@ -60,6 +60,10 @@ struct PackedScene {
     uint32_t ntri = 0, ntri_padded = 0;
     // materials: 8 floats each: (kind bits, r, g, b, param, 0, 0, 0)
     std::vector<float> mats;
+    // per-sphere shading record (one round trip after the hit): 8 floats
+    // (cx, cy, cz, r, colour r, g, b, fuzz|ir) + material kind
+    std::vector<float> sph_shade;
+    std::vector<uint32_t> sph_kind;
 };
 PackedScene pack_scene(const SceneModel &s, uint32_t sphere_pad, uint32_t tri_pad);
 

@@ -68,19 +68,20 @@ class RenderStats(C.Structure):
                 for k, t in self._fields_}
 
 
-_lib = None
+_libs = {}
 
 
 def build():
     subprocess.run(["make", "-s", "-C", HERE], check=True)
 
 
-def lib():
-    global _lib
-    if _lib is None:
-        if not os.path.exists(LIB_PATH):
-            raise RenderError(f"{LIB_PATH} is missing: run `make -C {HERE}` (build())")
-        L = C.CDLL(LIB_PATH)
+def lib(path=None):
+    """The loaded library (another build can be loaded side by side for A/B runs)."""
+    path = path or LIB_PATH
+    if path not in _libs:
+        if not os.path.exists(path):
+            raise RenderError(f"{path} is missing: run `make -C {HERE}` (build())")
+        L = C.CDLL(path)
         fp = C.POINTER(C.c_float)
         H = C.POINTER(WorldHandle)
         L.load_world.restype = H
@@ -119,8 +120,8 @@ def lib():
         L.rt_write_ppm.restype = C.c_int
         L.rt_write_ppm.argtypes = [C.POINTER(CFramebuffer), C.c_char_p]
         L.rt_device_count.restype = C.c_int
-        _lib = L
-    return _lib
+        _libs[path] = L
+    return _libs[path]
 
 
 def last_error() -> str:
@@ -144,9 +145,9 @@ def sample_seed(seed: int, job: int) -> int:
 
 
 def options(spp=16, depth=8, mode=RNG_COUNTER, seed=DEFAULT_SEED, replay=None, row_block=1,
-            rank=0, nranks=1, device=-1, accel=ACCEL_AUTO):
+            rank=0, nranks=1, device=-1, accel=ACCEL_AUTO, L=None):
     o = RenderOptions()
-    lib().rt_default_options(C.byref(o))
+    (L or lib()).rt_default_options(C.byref(o))
     o.samples_per_pixel, o.max_ray_bounces, o.rng_mode, o.seed = spp, depth, mode, seed
     o.row_block, o.rank, o.nranks, o.device = row_block, rank, nranks, device
     o.accel = accel
@@ -160,19 +161,24 @@ def options(spp=16, depth=8, mode=RNG_COUNTER, seed=DEFAULT_SEED, replay=None, r
 class World:
     """A loaded world: load_world (lib.rs:37-46) + camera moves + rendering."""
 
-    def __init__(self, source: str | bytes):
+    def __init__(self, source: str | bytes, lib_path=None):
+        self._L = lib(lib_path)
         if isinstance(source, str):
             source = source.encode("utf-8")
-        self._h = lib().load_world(source)
+        self._h = self._L.load_world(source)
         if not self._h:
-            raise ValueError(f"load_world failed: parse error {lib().rt_last_parse_error()}")
+            raise ValueError(f"load_world failed: parse error {self._L.rt_last_parse_error()}")
 
     def close(self):
         if getattr(self, "_h", None):
-            lib().rt_free_world(self._h)
+            self._L.rt_free_world(self._h)
             self._h = None
 
-    __del__ = close
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
     @property
     def handle(self):
@@ -180,75 +186,76 @@ class World:
 
     @property
     def num_spheres(self):
-        return int(lib().rt_world_num_spheres(self._h))
+        return int(self._L.rt_world_num_spheres(self._h))
 
     @property
     def num_triangles(self):
-        return int(lib().rt_world_num_triangles(self._h))
+        return int(self._L.rt_world_num_triangles(self._h))
 
     def spheres(self):
         out = np.zeros((self.num_spheres, 10), np.float32)
         for i in range(self.num_spheres):
-            lib().rt_world_sphere(self._h, i, out[i].ctypes.data_as(C.POINTER(C.c_float)))
+            self._L.rt_world_sphere(self._h, i, out[i].ctypes.data_as(C.POINTER(C.c_float)))
         return out
 
     def triangles(self):
         out = np.zeros((self.num_triangles, 18), np.float32)
         for i in range(self.num_triangles):
-            lib().rt_world_triangle(self._h, i, out[i].ctypes.data_as(C.POINTER(C.c_float)))
+            self._L.rt_world_triangle(self._h, i, out[i].ctypes.data_as(C.POINTER(C.c_float)))
         return out
 
     def camera(self):
         c = np.zeros(12, np.float32)
-        lib().rt_camera_get(self._h.contents.camera, c.ctypes.data_as(C.POINTER(C.c_float)))
+        self._L.rt_camera_get(self._h.contents.camera, c.ctypes.data_as(C.POINTER(C.c_float)))
         return c
 
     def move_camera(self, x, y, z):
         """GameView.swift:200-216: handle.camera = move_camera_position(camera, ...)."""
-        self._h.contents.camera = lib().move_camera_position(self._h.contents.camera, x, y, z)
+        self._h.contents.camera = self._L.move_camera_position(self._h.contents.camera, x, y, z)
 
     def render_reference(self, width, height):
         """The reference ABI call render(fb, handle): 16 spp, depth 8 (lib.rs:49-57)."""
         px = np.zeros((height, width, 4), np.uint8)
         fb = CFramebuffer(width, height, px.ctypes.data_as(C.POINTER(ColorU8)))
-        res = lib().render(fb, self._h)
+        res = self._L.render(fb, self._h)
         if not res.pixels and width * height:
-            raise RenderError(last_error())
+            raise RenderError(self._L.rt_last_error().decode())
         return px
 
     def render(self, width, height, spp=16, depth=8, mode=RNG_COUNTER, seed=DEFAULT_SEED,
                replay=None, row_block=1, rank=0, nranks=1, device=-1, accel=ACCEL_AUTO):
         """rt_render_ex -> (rgba uint8[tile_rows, width, 4], stats dict)."""
-        o, keep = options(spp, depth, mode, seed, replay, row_block, rank, nranks, device, accel)
-        rows = tile_rows(height, row_block, rank, nranks) if nranks > 1 else height
+        o, keep = options(spp, depth, mode, seed, replay, row_block, rank, nranks, device, accel,
+                          self._L)
+        rows = int(self._L.rt_tile_rows(height, row_block, rank, nranks)) if nranks > 1 else height
         px = np.zeros((rows, width, 4), np.uint8)
         fb = CFramebuffer(width, height, px.ctypes.data_as(C.POINTER(ColorU8)))
         st = RenderStats()
-        rc = lib().rt_render_ex(fb, self._h, C.byref(o), C.byref(st))
+        rc = self._L.rt_render_ex(fb, self._h, C.byref(o), C.byref(st))
         del keep
         if rc != 0:
-            raise RenderError(f"rt_render_ex failed ({rc}): {last_error()}")
+            raise RenderError(f"rt_render_ex failed ({rc}): {self._L.rt_last_error().decode()}")
         return px, st.as_dict()
 
     def read_samples(self, njobs, device=-1):
         """Per-sample colours of the last trace launch: float32[njobs, 4]."""
         out = np.zeros((njobs, 4), np.float32)
-        n = lib().rt_read_samples(self._h, device, out.ctypes.data_as(C.POINTER(C.c_float)),
+        n = self._L.rt_read_samples(self._h, device, out.ctypes.data_as(C.POINTER(C.c_float)),
                                   out.size)
         if n < 0:
-            raise RenderError(f"rt_read_samples failed ({n}): {last_error()}")
+            raise RenderError(f"rt_read_samples failed ({n}): {self._L.rt_last_error().decode()}")
         return out[: n // 4]
 
     def render_device(self, width, height, out_ptr: int, stream_ptr: int = 0, spp=16, depth=8,
                       mode=RNG_COUNTER, seed=DEFAULT_SEED, row_block=1, rank=0, nranks=1,
                       device=-1, accel=ACCEL_AUTO):
         """rt_render_device into a device buffer (e.g. a torch uint8 tensor)."""
-        o, _ = options(spp, depth, mode, seed, None, row_block, rank, nranks, device, accel)
+        o, _ = options(spp, depth, mode, seed, None, row_block, rank, nranks, device, accel, self._L)
         st = RenderStats()
-        rc = lib().rt_render_device(self._h, width, height, C.byref(o), C.c_void_p(out_ptr),
+        rc = self._L.rt_render_device(self._h, width, height, C.byref(o), C.c_void_p(out_ptr),
                                     C.c_void_p(stream_ptr or None), C.byref(st))
         if rc != 0:
-            raise RenderError(f"rt_render_device failed ({rc}): {last_error()}")
+            raise RenderError(f"rt_render_device failed ({rc}): {self._L.rt_last_error().decode()}")
         return st.as_dict()
 
 

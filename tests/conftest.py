@@ -5,7 +5,7 @@ import sys
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-PKG = os.path.join(ROOT, "rust-swift-raytracer_amd")
+PKG = os.path.join(ROOT, "rust-swift-raytracer_amd")  # noqa
 for p in (PKG, os.path.join(ROOT, "oracle"), os.path.join(ROOT, "tools"),
           os.path.join(ROOT, "tests")):
     if p not in sys.path:
