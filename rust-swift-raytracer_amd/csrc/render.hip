@@ -293,13 +293,17 @@ __global__ __launch_bounds__(kLds ? 512 : 256) void trace_kernel(TraceParams p) 
     uint32_t pool_next = 0, pool_end = 0;  // wave-uniform job pool
     bool exhausted = false;
 
+    uint32_t prefetch = 0;         // lane 0: base of the next chunk, fetched early
+    bool prefetch_pending = false;  // wave-uniform
     for (;;) {
         // ---- refill lanes whose path ended (active-ray compaction) -------
         const uint64_t dead = __ballot(!active);
-        if (dead != 0 && !exhausted) {
+        const uint32_t ndead = (uint32_t)__popcll(dead);
+        if (dead != 0 && !exhausted && (ndead >= p.refill_min || ndead == kWave)) {
             if (pool_next >= pool_end) {
-                uint32_t base = 0;
-                if (lane == 0) base = atomicAdd(p.job_counter, p.chunk);
+                uint32_t base = prefetch;
+                if (!prefetch_pending && lane == 0) base = atomicAdd(p.job_counter, p.chunk);
+                prefetch_pending = false;
                 base = __builtin_amdgcn_readfirstlane(base);
                 if (base >= p.njobs) {
                     exhausted = true;
@@ -337,7 +341,13 @@ __global__ __launch_bounds__(kLds ? 512 : 256) void trace_kernel(TraceParams p) 
                 bounce = 0;
                 active = true;
             }
-            pool_next += min((uint32_t)__popcll(dead), avail);
+            pool_next += min(ndead, avail);
+            // ask for the next chunk now; the reply is only waited for when the
+            // pool runs dry (hides the ~1-3 us atomic round trip)
+            if (!exhausted && !prefetch_pending && pool_end - pool_next < kWave) {
+                if (lane == 0) prefetch = atomicAdd(p.job_counter, p.chunk);
+                prefetch_pending = true;
+            }
         }
         if (__ballot(active) == 0) {
             if (exhausted) break;
@@ -410,18 +420,23 @@ __global__ __launch_bounds__(kLds ? 512 : 256) void trace_kernel(TraceParams p) 
                     nrm = unit(divide(pos - f3(S.x, S.y, S.z), S.w));  // common.rs:95
                     cr = M.x; cg = M.y; cb = M.z; param = M.w;
                 }
-                bool next = true;
-                F3 ndir;
-                if (kind == kMatDiffuse) {  // materials.rs:42-52
-                    const F3 sc = nrm + draw_unit(rng);
-                    const float e = 1e-8f;
-                    const bool nz = fabsf(sc.x) < e && fabsf(sc.y) < e && fabsf(sc.z) < e;
-                    ndir = nz ? nrm : unit(sc);
-                } else if (kind == kMatMetal) {  // materials.rs:54-63
-                    const F3 refl = dir - scale(nrm, 2.0f * dot(dir, nrm));
-                    const F3 d2 = refl + scale(draw_unit(rng), param);
-                    next = dot(d2, nrm) >= 0.0f;
-                    ndir = unit(d2);
+                // Each scatter builds an un-normalised direction `v`; the draws
+                // of diffuse and metal (random_unit_sphere, common.rs:32-38) and
+                // the final normalisation are shared code so divergent lanes do
+                // not execute three copies of the divide/sqrt sequences.
+                bool next = true, keep_normal = false;
+                F3 v = nrm;
+                if (kind == kMatDiffuse || kind == kMatMetal) {
+                    const F3 ru = draw_unit(rng);
+                    if (kind == kMatDiffuse) {  // materials.rs:42-52
+                        v = nrm + ru;
+                        const float e = 1e-8f;
+                        keep_normal = fabsf(v.x) < e && fabsf(v.y) < e && fabsf(v.z) < e;
+                    } else {  // materials.rs:54-63 (reflect, maths.rs:26-28)
+                        const F3 refl = dir - scale(nrm, 2.0f * dot(dir, nrm));
+                        v = refl + scale(ru, param);
+                        next = dot(v, nrm) >= 0.0f;
+                    }
                 } else if (kind == kMatDielectric) {  // materials.rs:65-97
                     F3 n2 = nrm;
                     float eta = param;
@@ -429,7 +444,7 @@ __global__ __launch_bounds__(kLds ? 512 : 256) void trace_kernel(TraceParams p) 
                     const float cos_t = dot(-dir, n2);  // maths.rs:31-36
                     const F3 perp = scale(dir + scale(n2, cos_t), eta);
                     const F3 par = scale(n2, -__builtin_sqrtf(fabsf(1.0f - dot(perp, perp))));
-                    ndir = unit(perp + par);
+                    v = perp + par;
                     cr = cg = cb = 1.0f;
                 } else {  // Emission (materials.rs:100-102)
                     next = false;
@@ -439,7 +454,7 @@ __global__ __launch_bounds__(kLds ? 512 : 256) void trace_kernel(TraceParams p) 
                     thr_g = thr_g * cg;
                     thr_b = thr_b * cb;
                     org = pos;
-                    dir = ndir;
+                    dir = keep_normal ? nrm : unit(v);
                     ++bounce;
                 } else {  // common.rs:273-274: final * colour
                     out_r = thr_r * cr;

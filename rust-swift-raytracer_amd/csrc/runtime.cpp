@@ -225,6 +225,7 @@ int render_frame(WorldState &w, const CameraModel &cam, size_t width, size_t hei
     p.div_spp = make_fastdiv(spp);
     p.div_width = make_fastdiv((uint32_t)width);
     p.div_rowblock = make_fastdiv(B);
+    p.refill_min = (uint32_t)std::max<uint64_t>(1, env_u64("RT_AMD_REFILL", 1));
     p.row_block = B; p.rank = o.rank; p.nranks = nranks;
     const bool use_bvh = d->nnodes > 0 && o.accel != RT_ACCEL_BRUTE;
     if (use_bvh) {
