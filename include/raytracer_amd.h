@@ -59,6 +59,9 @@ typedef struct RtRenderStats {
   uint64_t bvh_sphere_tests; /* sphere tests executed inside the BVH         */
   uint64_t bvh_node_tests;   /* BVH node (box) tests executed                */
   uint64_t big_sphere_tests; /* rays * spheres kept out of the BVH           */
+  uint64_t stamp_cycles[4];  /* diagnostic builds (-DRT_STAMPS) only: wave
+                                cycles in refill / sphere search / shading /
+                                store; zero in the product build             */
 } RtRenderStats;
 
 /* spp 16, depth 8 (lib.rs:51), COUNTER, seed 2547549, one rank, device -1. */

@@ -47,7 +47,7 @@ struct TraceParams {
     uint32_t ablate;          // timing-only diagnostics (RT_AMD_ABLATE): 1 = skip the tree walk
     const float4 *sph_shade;  // 2 per sphere: (centre, r) (colour, fuzz|ir)
     const uint32_t *sph_kind; // material kind per sphere
-    FastDiv div_spp, div_width, div_rowblock;  // job -> pixel mapping
+    FastDiv div_npix, div_width, div_rowblock;  // job -> (sample, pixel) mapping
     uint32_t refill_min;      // refill dead lanes once at least this many are idle
     float bvh_c[3], bvh_r, bvh_rmax, bvh_mag;
 };

@@ -293,6 +293,23 @@ __global__ __launch_bounds__(kLds ? 512 : 256) void trace_kernel(TraceParams p) 
     uint32_t pool_next = 0, pool_end = 0;  // wave-uniform job pool
     bool exhausted = false;
 
+#ifdef RT_STAMPS
+    // diagnostic build only: wave cycles per loop segment (s_memtime deltas)
+    uint64_t stamp_acc[4] = {0, 0, 0, 0};
+    uint64_t stamp_prev = __builtin_amdgcn_s_memtime();
+#define RT_STAMP(k)                                                       \
+    do {                                                                  \
+        __builtin_amdgcn_sched_barrier(0);                                \
+        const uint64_t t_ = __builtin_amdgcn_s_memtime();                 \
+        __builtin_amdgcn_sched_barrier(0);                                \
+        stamp_acc[k] += t_ - stamp_prev;                                  \
+        stamp_prev = t_;                                                  \
+    } while (0)
+#else
+#define RT_STAMP(k) \
+    do {            \
+    } while (0)
+#endif
     uint32_t prefetch = 0;         // lane 0: base of the next chunk, fetched early
     bool prefetch_pending = false;  // wave-uniform
     for (;;) {
@@ -317,10 +334,14 @@ __global__ __launch_bounds__(kLds ? 512 : 256) void trace_kernel(TraceParams p) 
                 (uint32_t)(dead >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)dead, 0u));
             if (!active && rank < avail) {
                 const uint32_t job = pool_next + rank;
-                // job -> (tile row, column, sample) -> reference (row, col)
-                const uint32_t lp = fdiv(job, p.div_spp);
-                const uint32_t s = job - lp * p.spp;
-                slot = s * p.npix + lp;  // sample-major slab: resolve reads coalesce
+                // Jobs are enumerated sample-major (job = s*npix + pixel): a
+                // wave's lanes trace neighbouring pixels and store their
+                // colours to consecutive slab slots, and the resolve reads
+                // coalesce.  Seeds and replay states use the reference's job
+                // index below, so the enumeration order changes no bits.
+                const uint32_t s = fdiv(job, p.div_npix);
+                const uint32_t lp = job - s * p.npix;
+                slot = job;
                 const uint32_t q = fdiv(lp, p.div_width);
                 const uint32_t col = lp - q * p.width;
                 const uint32_t lr = p.slab_row0 + q;
@@ -349,6 +370,7 @@ __global__ __launch_bounds__(kLds ? 512 : 256) void trace_kernel(TraceParams p) 
                 prefetch_pending = true;
             }
         }
+        RT_STAMP(0);
         if (__ballot(active) == 0) {
             if (exhausted) break;
             continue;
@@ -370,6 +392,7 @@ __global__ __launch_bounds__(kLds ? 512 : 256) void trace_kernel(TraceParams p) 
             } else {
                 spheres_brute(p, org, dir, best_t, best_i);
             }
+            RT_STAMP(1);
             // Mesh::hit with t_max = best_t, own closest from +inf (common.rs:178-223)
             float tri_t = __builtin_inff();
             int tri_i = -1;
@@ -464,13 +487,19 @@ __global__ __launch_bounds__(kLds ? 512 : 256) void trace_kernel(TraceParams p) 
                 }
             }
         }
+        RT_STAMP(2);
         if (done) {
             p.samples[slot] = make_float4(out_r, out_g, out_b, 0.0f);
             active = false;
         }
+        RT_STAMP(3);
     }
 
     // ---- per-wave statistics: one atomic per counter per wave ------------
+#ifdef RT_STAMPS
+    if (lane == 0)
+        for (int k = 0; k < 4; ++k) atomicAdd(&p.stats[4 + k], (unsigned long long)stamp_acc[k]);
+#endif
     uint64_t c[4] = {rays, tri_in, sph_tests, node_tests};
 #pragma unroll
     for (int k = 0; k < 4; ++k)

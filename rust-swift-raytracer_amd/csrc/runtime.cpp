@@ -201,7 +201,7 @@ int render_frame(WorldState &w, const CameraModel &cam, size_t width, size_t hei
         HIP_TRY(grow(d->replay, d->replay_cap, n));
         HIP_TRY(hipMemcpyAsync(d->replay, o.replay_states, n * 4, hipMemcpyHostToDevice, s));
     }
-    HIP_TRY(hipMemsetAsync(d->stats, 0, 32, s));
+    HIP_TRY(hipMemsetAsync(d->stats, 0, 64, s));
 
     TraceParams p{};
     p.sph_hot = d->sph_hot; p.sph_cold = d->sph_cold;
@@ -222,7 +222,7 @@ int render_frame(WorldState &w, const CameraModel &cam, size_t width, size_t hei
     p.ablate = (uint32_t)env_u64("RT_AMD_ABLATE", 0);
     p.sph_shade = d->sph_shade;
     p.sph_kind = d->sph_kind;
-    p.div_spp = make_fastdiv(spp);
+
     p.div_width = make_fastdiv((uint32_t)width);
     p.div_rowblock = make_fastdiv(B);
     p.refill_min = (uint32_t)std::max<uint64_t>(1, env_u64("RT_AMD_REFILL", 1));
@@ -252,6 +252,7 @@ int render_frame(WorldState &w, const CameraModel &cam, size_t width, size_t hei
         p.slab_row0 = (uint32_t)r0;
         p.njobs = (uint32_t)njobs;
         p.npix = (uint32_t)(rows * width);
+        p.div_npix = make_fastdiv(p.npix);
         HIP_TRY(hipEventRecord(d->ev[0], s));
         if (njobs) {
             const uint64_t jobs_per_block = waves_per_block * 256;
@@ -278,8 +279,8 @@ int render_frame(WorldState &w, const CameraModel &cam, size_t width, size_t hei
         trace_ms += a;
         resolve_ms += b;
     }
-    unsigned long long st[4] = {0, 0, 0, 0};
-    HIP_TRY(hipMemcpyAsync(st, d->stats, 32, hipMemcpyDeviceToHost, s));
+    unsigned long long st[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    HIP_TRY(hipMemcpyAsync(st, d->stats, 64, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
     if (stats) {
         stats->samples = (uint64_t)T * jobs_per_row;
@@ -295,6 +296,7 @@ int render_frame(WorldState &w, const CameraModel &cam, size_t width, size_t hei
         stats->bvh_sphere_tests = st[2];
         stats->bvh_node_tests = st[3];
         stats->big_sphere_tests = use_bvh ? st[0] * (uint64_t)d->nbig : st[0] * (uint64_t)d->nsph;
+        for (int k = 0; k < 4; ++k) stats->stamp_cycles[k] = st[4 + k];
     }
     return 0;
 }

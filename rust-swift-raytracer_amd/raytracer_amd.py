@@ -61,11 +61,14 @@ class RenderStats(C.Structure):
                 ("trace_ms", C.c_double), ("resolve_ms", C.c_double),
                 ("trace_launches", C.c_uint32), ("waves", C.c_uint32), ("accel", C.c_uint32),
                 ("bvh_sphere_tests", C.c_uint64), ("bvh_node_tests", C.c_uint64),
-                ("big_sphere_tests", C.c_uint64)]
+                ("big_sphere_tests", C.c_uint64), ("stamp_cycles", C.c_uint64 * 4)]
 
     def as_dict(self):
-        return {k: (float(getattr(self, k)) if t is C.c_double else int(getattr(self, k)))
-                for k, t in self._fields_}
+        out = {}
+        for k, t in self._fields_:
+            v = getattr(self, k)
+            out[k] = float(v) if t is C.c_double else list(v) if k == "stamp_cycles" else int(v)
+        return out
 
 
 _libs = {}

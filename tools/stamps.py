@@ -1,0 +1,25 @@
+"""Segment shares of the trace kernel from a -DRT_STAMPS diagnostic build
+(ab/stamps/libraytracer.so): wave cycles spent in refill / sphere search /
+shading / store+loop.  Read the SHARES, never the run time (stamps fence the
+schedule).  usage: python tools/stamps.py [config] [lib]"""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "rust-swift-raytracer_amd"))
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+import raytracer_amd as R  # noqa: E402
+import scenes as S  # noqa: E402
+
+cfg = sys.argv[1] if len(sys.argv) > 1 else "c2"
+path = sys.argv[2] if len(sys.argv) > 2 else os.path.join(ROOT, "ab", "stamps", "libraytracer.so")
+make, W, H, spp, depth = S.CONFIGS[cfg]
+w = R.World(make(), lib_path=path)
+for accel in (R.ACCEL_BVH, R.ACCEL_BRUTE):
+    w.render(W, H, spp, depth, accel=accel)
+    _, st = w.render(W, H, spp, depth, accel=accel)
+    c = st["stamp_cycles"]
+    tot = sum(c)
+    print(cfg, "accel", accel, "trace_ms %.3f" % st["trace_ms"], "shares:",
+          " ".join(f"{n}={x / tot:.3f}" for n, x in zip(["refill", "spheres", "shade", "store"], c)),
+          "cycles/ray %.0f" % (tot / st["rays"]))
