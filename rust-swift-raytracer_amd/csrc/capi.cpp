@@ -3,6 +3,7 @@
 // MacOSPlatform/MacOSPlatform/Engine/includes/raytracer.h:42-47) plus the
 // extensions declared in include/raytracer_amd.h.
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 
@@ -48,7 +49,9 @@ Rust_WorldHandle *load_world(const char *source) {
     }
     // spheres padded to the kernel's scalar-load batch of 8 with NaN centres
     world->state.packed = rtamd::pack_scene(world->state.scene, 8, 1);
-    world->state.bvh = rtamd::build_sphere_bvh(world->state.scene.spheres, 2);
+    const char *leaf = std::getenv("RT_AMD_LEAF");  // tuning knob: spheres per BVH leaf
+    world->state.bvh = rtamd::build_sphere_bvh(world->state.scene.spheres,
+                                               leaf ? (uint32_t)std::atoi(leaf) : 2u);
     auto *cam = new Rust_Camera{world->state.scene.camera};
     return new Rust_WorldHandle{world, cam};
 }

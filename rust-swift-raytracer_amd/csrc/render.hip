@@ -163,11 +163,6 @@ __device__ __forceinline__ bool sphere_candidate(float4 S, F3 org, F3 dir, int i
     return take;
 }
 
-// Slab bounds widened by 1e-6 relative (covers the ~3 ulp error of the slab
-// arithmetic) so that a box is only pruned when it is certainly missed.
-__device__ __forceinline__ float lower_rel(float x) { return x * (x > 0.0f ? 0.999999f : 1.000001f); }
-__device__ __forceinline__ float upper_rel(float x) { return x * (x > 0.0f ? 1.000001f : 0.999999f); }
-
 constexpr float kErrK = 3.0e-3f;  // >= 2.7x the derived sqrt(30u) = 1.12e-3
 
 // Where the traversal reads the tree from: global memory (any size) or the
@@ -217,17 +212,22 @@ __device__ __forceinline__ void spheres_bvh(const TraceParams &p, const BvhView 
         const float4 B0 = v.nodes[2 * node];
         const float4 B1 = v.nodes[2 * node + 1];
         const uint32_t miss = kLds ? (uint32_t)v.miss16[8 * node + oct] : v.miss32[8 * node + oct];
+        // Each computed slab value is (b - lo)(1+d1) * inv(1+d2)(1+d3): the
+        // exact value for a face moved by <= 3u|b - lo|, which e_abs covers,
+        // so [tn, tf] is the exact interval of a box that still contains
+        // every inflated sphere of the node: plain comparisons are safe.
         const float t0x = (B0.x - lo.x) * ix, t1x = (B1.x - hi.x) * ix;
         const float t0y = (B0.y - lo.y) * iy, t1y = (B1.y - hi.y) * iy;
         const float t0z = (B0.z - lo.z) * iz, t1z = (B1.z - hi.z) * iz;
         const float tn = fmaxf(fmaxf(fminf(t0x, t1x), fminf(t0y, t1y)), fminf(t0z, t1z));
         const float tf = fminf(fminf(fmaxf(t0x, t1x), fmaxf(t0y, t1y)), fmaxf(t0z, t1z));
-        const bool skip = lower_rel(tn) > upper_rel(tf) || upper_rel(tf) < 0.001f ||
-                          lower_rel(tn) > upper_rel(best_t);
+        // NaN (0 * inf on a degenerate slab) compares false: never a skip
+        const bool skip = tn > tf || tf < 0.001f || tn > best_t;
         const uint32_t a = __float_as_uint(B0.w);
-        if (skip) {
-            node = miss;
-        } else if (a & kLeafBitDev) {
+        const bool leaf = (a & kLeafBitDev) != 0;
+        const uint32_t child = a + ((oct >> __float_as_uint(B1.w)) & 1u);  // near child first
+        const uint32_t next = (skip || leaf) ? miss : child;
+        if (!skip && leaf) {
             const uint32_t first = a & ~kLeafBitDev, count = __float_as_uint(B1.w);
             bool changed = false;
             for (uint32_t j = first; j < first + count; ++j) {
@@ -239,10 +239,8 @@ __device__ __forceinline__ void spheres_bvh(const TraceParams &p, const BvhView 
                 lo = f3(org.x + e, org.y + e, org.z + e);
                 hi = f3(org.x - e, org.y - e, org.z - e);
             }
-            node = miss;
-        } else {
-            node = a + ((oct >> __float_as_uint(B1.w)) & 1u);  // near child first
         }
+        node = next;
     }
 }
 

@@ -46,7 +46,14 @@ def main():
         parts = rest.split(":")
         path = os.path.join(ROOT, parts[0]) if not os.path.isabs(parts[0]) else parts[0]
         env = dict(kv.split("=", 1) for kv in parts[1:])
+        saved = {k: os.environ.get(k) for k in env}
+        os.environ.update(env)  # load-time knobs (e.g. RT_AMD_LEAF) too
         variants.append((label, R.World(src, lib_path=path), env))
+        for k, v in saved.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
     res = {label: {"trace": [], "frame": [], "rays": 0} for label, _, _ in variants}
     for rnd in range(args.rounds + 1):
         for label, world, env in variants:
