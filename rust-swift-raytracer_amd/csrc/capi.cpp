@@ -51,7 +51,7 @@ Rust_WorldHandle *load_world(const char *source) {
     world->state.packed = rtamd::pack_scene(world->state.scene, 8, 1);
     const char *leaf = std::getenv("RT_AMD_LEAF");  // tuning knob: spheres per BVH leaf
     world->state.bvh = rtamd::build_sphere_bvh(world->state.scene.spheres,
-                                               leaf ? (uint32_t)std::atoi(leaf) : 2u);
+                                               leaf ? (uint32_t)std::atoi(leaf) : 3u);
     auto *cam = new Rust_Camera{world->state.scene.camera};
     return new Rust_WorldHandle{world, cam};
 }
