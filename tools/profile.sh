@@ -19,7 +19,6 @@ BENCH_ARGS=("$@")
 run trace 600 --kernel-trace --stats
 run pmc_fetch 600 --kernel-trace --pmc FETCH_SIZE
 run pmc_write 600 --kernel-trace --pmc WRITE_SIZE
-run pmc_valu 600 --kernel-trace --pmc SQ_INSTS_VALU SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE
-run pmc_wait 600 --kernel-trace --pmc SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS SQ_INSTS_SALU
-rocprofv3 -L > "$OUT/counters_list.txt" 2>&1 || true
+run pmc_valu 600 --kernel-trace --pmc SQ_INSTS_VALU SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_VALU SQ_INSTS_SALU
+run pmc_wait 600 --kernel-trace --pmc SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE
 find "$OUT" -name "*.csv" | head -20
