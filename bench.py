@@ -41,6 +41,9 @@ ROW_BLOCK = 8  # multi-GPU: row-cyclic blocks of 8 image rows
 
 
 NODE_TEST_FLOPS = 26  # slab test: 6 sub, 6 mul, 10 min/max, 4 slack mul/compare
+# triangle node: s = n^.o interval (6 mul, 6 min/max, 4 add), phantom offsets
+# (3 x [4 mul, 6 min/max, 2 mul, 4 add]), slab test (6 sub, 6 mul, 10 min/max, 3 cmp)
+TRI_NODE_TEST_FLOPS = 89
 
 
 def algorithmic_flops(st):
@@ -54,9 +57,12 @@ def algorithmic_flops(st):
 def executed_flops(st):
     """The same price list applied to the work the kernel actually executed:
     sphere tests done (BVH leaves + spheres kept out of the tree, or all of
-    them in brute force) plus NODE_TEST_FLOPS per BVH box test."""
+    them in brute force) plus NODE_TEST_FLOPS per BVH box test; triangle
+    tests done (leaves + brute-forced ones) plus TRI_NODE_TEST_FLOPS per
+    triangle-BVH box test."""
     sph = st["bvh_sphere_tests"] + st["big_sphere_tests"]
-    return (17 * sph + NODE_TEST_FLOPS * st["bvh_node_tests"] + 14 * st["tri_tests"]
+    return (17 * sph + NODE_TEST_FLOPS * st["bvh_node_tests"] + 14 * st["bvh_tri_tests"]
+            + TRI_NODE_TEST_FLOPS * st["tri_node_tests"]
             + 60 * st["tri_in_range"] + 40 * st["rays"] + 20 * st["samples"])
 
 
@@ -188,6 +194,9 @@ def main():
         "accel": {1: "brute", 2: "bvh"}.get(st0["accel"], "?"),
         "per_ray": {"sphere_tests": (st0["bvh_sphere_tests"] + st0["big_sphere_tests"]) / st0["rays"],
                     "node_tests": st0["bvh_node_tests"] / st0["rays"],
+                    "tri_tests": st0["bvh_tri_tests"] / st0["rays"],
+                    "tri_node_tests": st0["tri_node_tests"] / st0["rays"],
+                    "tri_in_range": st0["tri_in_range"] / st0["rays"],
                     "brute_force_sphere_tests": st0["sphere_tests"] / st0["rays"]},
     }
     if nr == 1 and not args.no_cpu_baseline:

@@ -41,7 +41,8 @@ typedef struct RtRenderOptions {
 
 /* Sphere search.  Both give bit-identical frames:
  *   RT_ACCEL_BRUTE: every sphere in file order (common.rs:241-247).
- *   RT_ACCEL_BVH:   exact-pruning BVH (falls back to BRUTE for < 16 spheres).
+ *   RT_ACCEL_BVH:   exact-pruning BVHs: spheres (BRUTE below 16 spheres) and
+ *                   the phantom-aware triangle tree (BRUTE below 16 triangles).
  *   RT_ACCEL_AUTO:  BVH when the scene has one, else BRUTE.  Default. */
 enum { RT_ACCEL_AUTO = 0, RT_ACCEL_BRUTE = 1, RT_ACCEL_BVH = 2 };
 
@@ -62,6 +63,10 @@ typedef struct RtRenderStats {
   uint64_t stamp_cycles[4];  /* diagnostic builds (-DRT_STAMPS) only: wave
                                 cycles in refill / sphere search / shading /
                                 store; zero in the product build             */
+  uint64_t tri_node_tests;   /* triangle-BVH node tests executed              */
+  uint64_t bvh_tri_tests;    /* triangle tests executed (== tri_tests brute)  */
+  uint32_t tri_bvh;          /* 1 when the triangle BVH ran                   */
+  uint32_t reserved;
 } RtRenderStats;
 
 /* spp 16, depth 8 (lib.rs:51), COUNTER, seed 2547549, one rank, device -1. */

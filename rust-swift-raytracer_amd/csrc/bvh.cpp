@@ -3,6 +3,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <limits>
 
@@ -28,7 +29,7 @@ struct Box {
     }
 };
 
-struct Prim { Box box; double c[3]; uint32_t id; };
+struct Prim { Box box; double c[3]; uint32_t id; double n[3] = {0, 0, 0}; };
 
 inline float down(double x) {  // largest float <= x
     float f = (float)x;
@@ -43,11 +44,28 @@ inline float bits_f(uint32_t u) { float f; std::memcpy(&f, &u, 4); return f; }
 struct Builder {
     std::vector<Prim> &prims;
     uint32_t leaf_size;
+    // phantom > 0: triangles.  A node's effective box is its box widened by
+    // the phantom offsets 2(n^.o)n^ over its normal box (bvh.h), so the SAH
+    // prices that widened box for |o| ~ phantom and may also split on the
+    // normal components (axes 3-5).
+    double phantom = 0;
     struct Node { Box box; uint32_t a = 0, b = 0; bool leaf = false; };
     std::vector<Node> nodes;
     uint32_t max_depth = 0;
 
-    Builder(std::vector<Prim> &p, uint32_t ls) : prims(p), leaf_size(ls) {}
+    Builder(std::vector<Prim> &p, uint32_t ls, double ph = 0) : prims(p), leaf_size(ls), phantom(ph) {}
+
+    double cost_area(const Box &g, const Box &n) const {
+        if (phantom <= 0) return g.area();
+        double dn[3], sum = 0, e[3];
+        for (int k = 0; k < 3; ++k) { dn[k] = std::max(0.0, n.hi[k] - n.lo[k]); sum += dn[k]; }
+        for (int k = 0; k < 3; ++k) {
+            const double mid = std::fabs(n.hi[k] + n.lo[k]) / 2;
+            e[k] = std::max(0.0, g.hi[k] - g.lo[k]) + 2 * phantom * (dn[k] + mid * sum);
+        }
+        return 2.0 * (e[0] * e[1] + e[1] * e[2] + e[2] * e[0]);
+    }
+    static double key(const Prim &p, int ax) { return ax < 3 ? p.c[ax] : p.n[ax - 3]; }
 
     void make_leaf(uint32_t n, uint32_t first, uint32_t count) {
         nodes[n].leaf = true;
@@ -58,45 +76,62 @@ struct Builder {
     // Builds node n over prims[first, first + count).
     void build(uint32_t n, uint32_t first, uint32_t count, uint32_t depth) {
         max_depth = std::max(max_depth, depth);
-        Box box, cbox;
-        for (uint32_t i = first; i < first + count; ++i) { box.grow(prims[i].box); cbox.grow(prims[i].c); }
+        Box box, cbox, nbox;
+        for (uint32_t i = first; i < first + count; ++i) {
+            box.grow(prims[i].box);
+            cbox.grow(prims[i].c);
+            nbox.grow(prims[i].n);
+        }
         nodes[n].box = box;
         if (count <= leaf_size) { make_leaf(n, first, count); return; }
-        // binned SAH over the centroid box
+        // binned SAH over the centroid box (and the normal box for triangles)
         constexpr int kBins = 16;
         double best_cost = std::numeric_limits<double>::infinity();
         int best_axis = -1, best_split = 0;
-        for (int ax = 0; ax < 3; ++ax) {
-            const double ext = cbox.hi[ax] - cbox.lo[ax];
+        double best_lo = 0, best_ext = 1;
+        const int naxes = phantom > 0 ? 6 : 3;
+        for (int ax = 0; ax < naxes; ++ax) {
+            const double lo = ax < 3 ? cbox.lo[ax] : nbox.lo[ax - 3];
+            const double ext = (ax < 3 ? cbox.hi[ax] : nbox.hi[ax - 3]) - lo;
             if (!(ext > 0)) continue;
-            Box bb[kBins];
+            Box bb[kBins], nb[kBins];
             uint32_t cnt[kBins] = {0};
             for (uint32_t i = first; i < first + count; ++i) {
-                int b = (int)((prims[i].c[ax] - cbox.lo[ax]) / ext * kBins);
+                int b = (int)((key(prims[i], ax) - lo) / ext * kBins);
                 b = std::min(kBins - 1, std::max(0, b));
                 bb[b].grow(prims[i].box);
+                nb[b].grow(prims[i].n);
                 ++cnt[b];
             }
-            Box left[kBins];
+            double left[kBins];
             uint32_t lc[kBins];
-            Box acc;
+            Box acc, nacc;
             uint32_t c = 0;
-            for (int b = 0; b < kBins; ++b) { acc.grow(bb[b]); c += cnt[b]; left[b] = acc; lc[b] = c; }
+            for (int b = 0; b < kBins; ++b) {
+                acc.grow(bb[b]);
+                nacc.grow(nb[b]);
+                c += cnt[b];
+                left[b] = cost_area(acc, nacc);
+                lc[b] = c;
+            }
             acc = Box();
+            nacc = Box();
             c = 0;
             for (int b = kBins - 1; b > 0; --b) {
                 acc.grow(bb[b]);
+                nacc.grow(nb[b]);
                 c += cnt[b];
                 if (lc[b - 1] == 0 || c == 0) continue;
-                const double cost = left[b - 1].area() * lc[b - 1] + acc.area() * c;
-                if (cost < best_cost) { best_cost = cost; best_axis = ax; best_split = b; }
+                const double cost = left[b - 1] * lc[b - 1] + cost_area(acc, nacc) * c;
+                if (cost < best_cost) {
+                    best_cost = cost; best_axis = ax; best_split = b; best_lo = lo; best_ext = ext;
+                }
             }
         }
         uint32_t mid;
-        int axis = best_axis;
-        if (axis < 0 || depth > 40) {
+        if (best_axis < 0 || depth > 40) {
             // degenerate centroids (or very deep): median split on the widest axis
-            axis = 0;
+            int axis = 0;
             double w = -1;
             for (int k = 0; k < 3; ++k)
                 if (cbox.hi[k] - cbox.lo[k] > w) { w = cbox.hi[k] - cbox.lo[k]; axis = k; }
@@ -104,15 +139,29 @@ struct Builder {
             std::nth_element(prims.begin() + first, prims.begin() + mid, prims.begin() + first + count,
                              [axis](const Prim &x, const Prim &y) { return x.c[axis] < y.c[axis]; });
         } else {
-            const double ext = cbox.hi[axis] - cbox.lo[axis];
             auto it = std::partition(prims.begin() + first, prims.begin() + first + count,
                                      [&](const Prim &p) {
-                                         int b = (int)((p.c[axis] - cbox.lo[axis]) / ext * kBins);
+                                         int b = (int)((key(p, best_axis) - best_lo) / best_ext * kBins);
                                          b = std::min(kBins - 1, std::max(0, b));
                                          return b < best_split;
                                      });
             mid = (uint32_t)(it - prims.begin());
             if (mid == first || mid == first + count) mid = first + count / 2;
+        }
+        // Traversal order: the kernel visits child a first unless the ray
+        // points down axis b.  b = the axis that best separates the children's
+        // mean centroids, with the lower child first.
+        double ml[3] = {0, 0, 0}, mr[3] = {0, 0, 0};
+        for (uint32_t i = first; i < mid; ++i)
+            for (int k = 0; k < 3; ++k) ml[k] += prims[i].c[k] / (mid - first);
+        for (uint32_t i = mid; i < first + count; ++i)
+            for (int k = 0; k < 3; ++k) mr[k] += prims[i].c[k] / (first + count - mid);
+        int axis = 0;
+        for (int k = 1; k < 3; ++k)
+            if (std::fabs(mr[k] - ml[k]) > std::fabs(mr[axis] - ml[axis])) axis = k;
+        if (ml[axis] > mr[axis]) {
+            std::rotate(prims.begin() + first, prims.begin() + mid, prims.begin() + first + count);
+            mid = first + (first + count - mid);
         }
         const uint32_t l = (uint32_t)nodes.size();
         nodes.emplace_back();
@@ -141,6 +190,144 @@ bool finite_sphere(const Sphere &s) {
 }
 
 }  // namespace
+
+// Box of the unit normals of prims in node n (recursive), rounded outward.
+static void normal_boxes(const Builder &b, const std::vector<Prim> &prims, uint32_t n,
+                         std::vector<Box> &out) {
+    Box nb;
+    const auto &nd = b.nodes[n];
+    if (nd.leaf) {
+        for (uint32_t i = nd.a; i < nd.a + nd.b; ++i) nb.grow(prims[i].n);
+    } else {
+        normal_boxes(b, prims, nd.a, out);
+        normal_boxes(b, prims, nd.a + 1, out);
+        nb.grow(out[nd.a]);
+        nb.grow(out[nd.a + 1]);
+    }
+    out[n] = nb;
+}
+
+TriangleBVH build_triangle_bvh(const std::vector<Triangle> &tris, const std::vector<float> &tri_hot,
+                               uint32_t leaf_size) {
+    TriangleBVH out;
+    std::vector<Prim> prims;
+    for (uint32_t i = 0; i < tris.size(); ++i) {
+        const Triangle &t = tris[i];
+        const double v[3][3] = {{t.v0.x, t.v0.y, t.v0.z}, {t.v1.x, t.v1.y, t.v1.z},
+                                {t.v2.x, t.v2.y, t.v2.z}};
+        const float *h = &tri_hot[(size_t)i * 4];
+        bool finite = std::isfinite(h[0]) && std::isfinite(h[1]) && std::isfinite(h[2]) &&
+                      std::isfinite(h[3]);
+        for (int k = 0; k < 3; ++k)
+            for (int j = 0; j < 3; ++j) finite = finite && std::isfinite(v[k][j]);
+        const double nn = std::sqrt((double)h[0] * h[0] + (double)h[1] * h[1] + (double)h[2] * h[2]);
+        if (finite && nn == 0.0) continue;  // cos == 0 for every finite ray: never accepted
+        // The edge tests accept points whose projection along the stored n lies
+        // in the triangle.  Keep only triangles whose stored n is within ~2.6
+        // degrees of the exact plane normal, so that projection is well
+        // conditioned; the rest (slivers, non-finite data) are brute forced.
+        double e1[3], e2[3], tn[3];
+        for (int k = 0; k < 3; ++k) { e1[k] = v[1][k] - v[0][k]; e2[k] = v[2][k] - v[0][k]; }
+        tn[0] = e1[1] * e2[2] - e1[2] * e2[1];
+        tn[1] = e1[2] * e2[0] - e1[0] * e2[2];
+        tn[2] = e1[0] * e2[1] - e1[1] * e2[0];
+        const double tl = std::sqrt(tn[0] * tn[0] + tn[1] * tn[1] + tn[2] * tn[2]);
+        const double cosphi = finite && tl > 0
+                                  ? (tn[0] * h[0] + tn[1] * h[1] + tn[2] * h[2]) / (tl * nn)
+                                  : -1.0;
+        if (!(cosphi >= 0.999)) { out.loose.push_back(i); continue; }
+        Prim p;
+        for (int k = 0; k < 3; ++k) p.n[k] = (double)h[k] / nn;
+        // Accepted points are q + (2 n^.o) n^ + w n^ with q in the triangle and
+        // |w| <= max_i |n^.(v0 - v_i)| (n^ is not exactly normal to the plane).
+        double w = 0;
+        for (int j = 1; j < 3; ++j) {
+            const double d = p.n[0] * (v[0][0] - v[j][0]) + p.n[1] * (v[0][1] - v[j][1]) +
+                             p.n[2] * (v[0][2] - v[j][2]);
+            w = std::max(w, std::fabs(d));
+        }
+        double vm = 0;
+        for (int k = 0; k < 3; ++k)
+            for (int j = 0; j < 3; ++j) vm = std::max(vm, std::fabs(v[k][j]));
+        w = w * (1 + 1e-9) + 1e-15 * vm;
+        for (int k = 0; k < 3; ++k) {
+            const double pad = w * std::fabs(p.n[k]);
+            p.box.lo[k] = std::min({v[0][k], v[1][k], v[2][k]}) - pad;
+            p.box.hi[k] = std::max({v[0][k], v[1][k], v[2][k]}) + pad;
+            p.c[k] = (p.box.lo[k] + p.box.hi[k]) / 2;
+        }
+        p.id = i;
+        prims.push_back(p);
+    }
+    if (prims.size() < 16) {  // not worth a tree: brute force keeps the reference order
+        out.loose.clear();
+        return out;
+    }
+    // phantom scale for the SAH: typical |o| (origins lie on or near the scene)
+    Box geo;
+    for (const Prim &p : prims) geo.grow(p.box);
+    double cn = 0, hd = 0;
+    for (int k = 0; k < 3; ++k) {
+        const double c = (geo.lo[k] + geo.hi[k]) / 2;
+        cn += c * c;
+        hd = std::max(hd, (geo.hi[k] - geo.lo[k]) / 2);
+    }
+    double L = 0.4 * (std::sqrt(cn) + hd / 2);  // A/B on C5 (tools/tbvh_sim.cpp): 1-4 best
+    if (const char *e = std::getenv("RT_AMD_TRI_PHANTOM")) L = std::atof(e);
+    Builder b(prims, std::max(1u, leaf_size), L > 0 ? L : 1e-30);
+    b.nodes.reserve(prims.size() * 2);
+    b.nodes.emplace_back();
+    b.build(0, 0, (uint32_t)prims.size(), 0);
+    out.depth = b.max_depth;
+    std::vector<Box> nbox(b.nodes.size());
+    normal_boxes(b, prims, 0, nbox);
+
+    Box all;
+    double mag = 0;
+    for (const Prim &p : prims) {
+        all.grow(p.box);
+        for (int k = 0; k < 3; ++k) mag = std::max({mag, std::fabs(p.box.lo[k]), std::fabs(p.box.hi[k])});
+    }
+    double half = 0;
+    for (int k = 0; k < 3; ++k) {
+        out.centre[k] = (float)((all.lo[k] + all.hi[k]) / 2);
+        half = std::max(half, std::max(all.hi[k] - out.centre[k], out.centre[k] - all.lo[k]));
+    }
+    out.radius = up(half * std::sqrt(3.0) * (1 + 1e-6));
+    out.mag = up(mag);
+
+    out.nodes.resize(b.nodes.size() * 16);
+    for (size_t n = 0; n < b.nodes.size(); ++n) {
+        const auto &nd = b.nodes[n];
+        float *o = &out.nodes[n * 16];
+        for (int k = 0; k < 3; ++k) {
+            o[k] = down(nd.box.lo[k]);
+            o[4 + k] = up(nd.box.hi[k]);
+            o[8 + k] = down(nbox[n].lo[k]);
+            o[12 + k] = up(nbox[n].hi[k]);
+        }
+        o[3] = bits_f(nd.leaf ? (nd.a | kLeafBit) : nd.a);
+        o[7] = bits_f(nd.b);
+    }
+    out.miss.assign(b.nodes.size() * 8, kNodeEnd);
+    for (uint32_t oct = 0; oct < 8; ++oct) b.links(0, kNodeEnd, oct, out.miss);
+    out.tris.resize(prims.size() * 16);
+    for (size_t i = 0; i < prims.size(); ++i) {
+        const uint32_t id = prims[i].id;
+        const Triangle &t = tris[id];
+        float *r = &out.tris[i * 16];
+        std::memcpy(r, &tri_hot[(size_t)id * 4], 4 * sizeof(float));
+        const Vec3 vs[3] = {t.v0, t.v1, t.v2};
+        for (int j = 0; j < 3; ++j) {
+            r[4 * (j + 1) + 0] = vs[j].x;
+            r[4 * (j + 1) + 1] = vs[j].y;
+            r[4 * (j + 1) + 2] = vs[j].z;
+            r[4 * (j + 1) + 3] = 0.0f;
+        }
+        r[7] = bits_f(id);
+    }
+    return out;
+}
 
 SphereBVH build_sphere_bvh(const std::vector<Sphere> &spheres, uint32_t leaf_size) {
     SphereBVH out;

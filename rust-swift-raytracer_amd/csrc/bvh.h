@@ -40,4 +40,28 @@ struct SphereBVH {
 
 SphereBVH build_sphere_bvh(const std::vector<Sphere> &spheres, uint32_t leaf_size);
 
+// Triangle BVH for Mesh::hit (common.rs:178-223).  The reference's triangle
+// t is (n.o + d)/cos (common.rs:141), so an accepted hit point lies on the
+// triangle translated by 2(n^.o)n^ -- a "phantom" copy that depends on the
+// ray origin o.  Each node therefore also stores the box of its triangles'
+// unit normals; the kernel widens the node box per ray by the interval of
+// 2(n^.o)n^ over that normal box plus a rounding margin.
+// Nodes: four float4 -- (min.xyz, a) (max.xyz, b) (nmin.xyz, 0) (nmax.xyz, 0)
+// with a/b as in SphereBVH.
+struct TriangleBVH {
+    std::vector<float> nodes;       // 16 floats per node
+    std::vector<uint32_t> miss;     // 8 per node
+    // 16 floats per BVH triangle, in tree order: (n.x, n.y, n.z, n.v0)
+    // (v0, bits(original index)) (v1, 0) (v2, 0)
+    std::vector<float> tris;
+    std::vector<uint32_t> loose;    // brute-forced triangles (non-finite data, slivers)
+    float centre[3] = {0, 0, 0};
+    float radius = 0, mag = 0;      // vertices within radius of centre; max |coordinate|
+    uint32_t depth = 0;
+};
+
+// tri_hot: PackedScene::tri_hot (the exact per-triangle n and n.v0 bits).
+TriangleBVH build_triangle_bvh(const std::vector<Triangle> &tris, const std::vector<float> &tri_hot,
+                               uint32_t leaf_size);
+
 }  // namespace rtamd

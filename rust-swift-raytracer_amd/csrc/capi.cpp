@@ -52,6 +52,10 @@ Rust_WorldHandle *load_world(const char *source) {
     const char *leaf = std::getenv("RT_AMD_LEAF");  // tuning knob: spheres per BVH leaf
     world->state.bvh = rtamd::build_sphere_bvh(world->state.scene.spheres,
                                                leaf ? (uint32_t)std::atoi(leaf) : 3u);
+    const char *tleaf = std::getenv("RT_AMD_TRI_LEAF");  // triangles per BVH leaf
+    world->state.tbvh = rtamd::build_triangle_bvh(world->state.scene.triangles,
+                                                  world->state.packed.tri_hot,
+                                                  tleaf ? (uint32_t)std::atoi(tleaf) : 4u);
     auto *cam = new Rust_Camera{world->state.scene.camera};
     return new Rust_WorldHandle{world, cam};
 }

@@ -21,7 +21,8 @@ struct TraceParams {
     const float *mats;        // 8 floats per material: kind bits, r, g, b, param
     float4 *samples;          // slab-local per-sample colour (r, g, b, 0)
     uint32_t *job_counter;    // zeroed before every launch
-    unsigned long long *stats;// rays, tri in t-range, BVH sphere tests, BVH node tests
+    unsigned long long *stats;// rays, tri in t-range, BVH sphere tests, BVH node tests,
+                              // 4 stamp counters, triangle-BVH node tests
     const uint32_t *replay;   // REPLAY start states (global job index)
     float cam[12];            // origin, lower_left, horizontal, vertical
     float wden, hden;         // (width-1) as f32, (height-1) as f32
@@ -50,6 +51,13 @@ struct TraceParams {
     FastDiv div_npix, div_width, div_rowblock;  // job -> (sample, pixel) mapping
     uint32_t refill_min;      // refill dead lanes once at least this many are idle
     float bvh_c[3], bvh_r, bvh_rmax, bvh_mag;
+    // phantom-aware triangle BVH (bvh.h TriangleBVH); tnodes == 0: brute-force Mesh loop
+    const float4 *tbvh_nodes; // 4 per node: (min, a) (max, b) (normal min) (normal max)
+    const uint32_t *tbvh_miss;// 8 per node
+    const float4 *tbvh_tris;  // 4 per triangle in tree order: (n, n.v0) (v0, id) (v1) (v2)
+    const uint32_t *tbvh_loose;  // triangles tested by brute force, ascending
+    uint32_t tnodes, ttris, tloose;
+    float tbvh_c[3], tbvh_r, tbvh_mag;
 };
 
 hipError_t launch_trace(const TraceParams &p, uint32_t blocks, hipStream_t stream);

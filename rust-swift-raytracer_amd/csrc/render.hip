@@ -244,6 +244,151 @@ __device__ __forceinline__ void spheres_bvh(const TraceParams &p, const BvhView 
     }
 }
 
+// ------------------------------------------------------------ triangle stage
+// Triangle::intersect (common.rs:129-166), after the t-range check passed:
+// the three edge tests against the hit point o + t*d.
+__device__ __forceinline__ bool tri_edges(F3 n, F3 v0, F3 v1, F3 v2, F3 pt) {
+    if (dot(n, cross(v1 - v0, pt - v0)) < 0.0f) return false;
+    if (dot(n, cross(v2 - v1, pt - v1)) < 0.0f) return false;
+    if (dot(n, cross(v0 - v2, pt - v2)) < 0.0f) return false;
+    return true;
+}
+
+// The reference's plane step and t-range check (common.rs:131-150), with its
+// sign: t = (n.o + d) / cos; false when |cos| < 1e-8 or t is out of range.
+__device__ __forceinline__ bool tri_plane(float4 N, F3 org, F3 dir, float best_t, float &t) {
+    const float cosl = (N.x * dir.x + N.y * dir.y) + N.z * dir.z;
+    if (-1e-8f < cosl && cosl < 1e-8f) return false;
+    t = (((N.x * org.x + N.y * org.y) + N.z * org.z) + N.w) / cosl;
+    return !(t < 0.001f || t > best_t);
+}
+
+// Mesh::hit (common.rs:178-223) in file order: t_max = best_t, first wins ties.
+__device__ __forceinline__ void triangles_brute(const TraceParams &p, F3 org, F3 dir, float best_t,
+                                                float &tri_t, int &tri_i, uint32_t &tri_in) {
+    const float tmin = 0.001f;
+    for (uint32_t j = 0; j < p.ntri; ++j) {
+        const float4 N = p.tri_hot[j];
+        const float cosl = (N.x * dir.x + N.y * dir.y) + N.z * dir.z;
+        if (-1e-8f < cosl && cosl < 1e-8f) continue;
+        const float t = (((N.x * org.x + N.y * org.y) + N.z * org.z) + N.w) / cosl;
+        if (t < tmin || t > best_t) continue;
+        ++tri_in;
+        const float4 *g = p.tri_geo + 4u * j;
+        const float4 A = g[0], B = g[1], Cc = g[2];
+        if (!tri_edges(f3(N.x, N.y, N.z), f3(A.x, A.y, A.z), f3(B.x, B.y, B.z), f3(Cc.x, Cc.y, Cc.z),
+                       org + scale(dir, t)))
+            continue;
+        if (t < tri_t) { tri_t = t; tri_i = (int)j; }
+    }
+}
+
+// One triangle in any order, with the reference's winner: the smallest
+// accepted t, lowest index on ties (a NaN/inf t is never recorded).
+__device__ __forceinline__ bool tri_merge(float t, int idx, float &tri_t, int &tri_i) {
+    const bool take = t < tri_t || (t == tri_t && tri_t < __builtin_inff() && idx < tri_i);
+    if (take) { tri_t = t; tri_i = idx; }
+    return take;
+}
+
+// One tree-ordered triangle record (bvh.h TriangleBVH::tris).
+__device__ __forceinline__ bool tri_record(const float4 *r, F3 org, F3 dir, float best_t,
+                                           float &tri_t, int &tri_i, uint32_t &tri_in) {
+    const float4 N = r[0];
+    float t;
+    if (!tri_plane(N, org, dir, best_t, t)) return false;
+    ++tri_in;
+    const float4 A = r[1], B = r[2], Cc = r[3];
+    if (!tri_edges(f3(N.x, N.y, N.z), f3(A.x, A.y, A.z), f3(B.x, B.y, B.z), f3(Cc.x, Cc.y, Cc.z),
+                   org + scale(dir, t)))
+        return false;
+    return tri_merge(t, (int)__float_as_uint(A.w), tri_t, tri_i);
+}
+
+// Triangles through the phantom-aware BVH (bvh.h).  An accepted hit lies on
+// its triangle translated by 2(n^.o)n^ (the reference's sign of n.o), up to
+// rounding.  Per node the kernel bounds s = n^.o over the node's normal box,
+// widens the box by the interval of 2 s m_k on each axis k (m over the normal
+// box) plus rho, a rounding margin that dominates every error term
+// (<= ~40u (dist + |o| + M)), and skips only nodes the ray
+// certainly misses or enters beyond min(best_t, tri_t).
+__device__ __forceinline__ void triangles_bvh(const TraceParams &p, F3 org, F3 dir, float best_t,
+                                              float &tri_t, int &tri_i, uint32_t &tri_in,
+                                              uint32_t &node_tests, uint32_t &tri_done) {
+    tri_done += p.tloose;
+    for (uint32_t k = 0; k < p.tloose; ++k) {  // slivers / non-finite data
+        const uint32_t j = p.tbvh_loose[k];
+        const float4 N = p.tri_hot[j];
+        float t;
+        if (!tri_plane(N, org, dir, best_t, t)) continue;
+        ++tri_in;
+        const float4 *g = p.tri_geo + 4u * j;
+        const float4 A = g[0], B = g[1], Cc = g[2];
+        if (tri_edges(f3(N.x, N.y, N.z), f3(A.x, A.y, A.z), f3(B.x, B.y, B.z), f3(Cc.x, Cc.y, Cc.z),
+                      org + scale(dir, t)))
+            tri_merge(t, (int)j, tri_t, tri_i);
+    }
+    const float onorm = (fabsf(org.x) + fabsf(org.y)) + fabsf(org.z);
+    if (!(onorm < 1e18f)) {
+        // far / non-finite origin: the margins below would overflow; every
+        // record is tested instead (order-independent merge, same result)
+        tri_done += p.ttris;
+        for (uint32_t j = 0; j < p.ttris; ++j)
+            tri_record(p.tbvh_tris + 4u * j, org, dir, best_t, tri_t, tri_i, tri_in);
+        return;
+    }
+    const float ix = 1.0f / dir.x, iy = 1.0f / dir.y, iz = 1.0f / dir.z;
+    const uint32_t oct = (ix < 0.0f ? 1u : 0u) | (iy < 0.0f ? 2u : 0u) | (iz < 0.0f ? 4u : 0u);
+    // distance from o to any phantom point: |o - c| + radius + 2|o|
+    const float dist = ((fabsf(org.x - p.tbvh_c[0]) + fabsf(org.y - p.tbvh_c[1])) +
+                        fabsf(org.z - p.tbvh_c[2])) + p.tbvh_r + 2.0f * onorm;
+    const float rho = 1e-5f * ((dist + onorm) + p.tbvh_mag);
+    float cap = fminf(best_t, tri_t);
+    uint32_t node = 0;
+    while (node != kNodeEndDev) {
+        ++node_tests;
+        const float4 *nd = p.tbvh_nodes + 4u * node;
+        const float4 B0 = nd[0], B1 = nd[1], N0 = nd[2], N1 = nd[3];
+        const uint32_t miss = p.tbvh_miss[8u * node + oct];
+        // s = n^.o over the normal box
+        const float ax = N0.x * org.x, bx = N1.x * org.x;
+        const float ay = N0.y * org.y, by = N1.y * org.y;
+        const float az = N0.z * org.z, bz = N1.z * org.z;
+        const float sl = (fminf(ax, bx) + fminf(ay, by)) + fminf(az, bz);
+        const float sh = (fmaxf(ax, bx) + fmaxf(ay, by)) + fmaxf(az, bz);
+        // phantom offset 2 s m_k over s in [sl, sh], m_k in [N0.k, N1.k]
+        auto widen = [&](float lo, float hi, float m0, float m1, float o, float inv, float &t0,
+                         float &t1) {
+            const float a = sl * m0, b = sl * m1, c = sh * m0, d = sh * m1;
+            const float omin = fminf(fminf(a, b), fminf(c, d));
+            const float omax = fmaxf(fmaxf(a, b), fmaxf(c, d));
+            const float l = (lo + 2.0f * omin) - rho;
+            const float h = (hi + 2.0f * omax) + rho;
+            t0 = (l - o) * inv;
+            t1 = (h - o) * inv;
+        };
+        float t0x, t1x, t0y, t1y, t0z, t1z;
+        widen(B0.x, B1.x, N0.x, N1.x, org.x, ix, t0x, t1x);
+        widen(B0.y, B1.y, N0.y, N1.y, org.y, iy, t0y, t1y);
+        widen(B0.z, B1.z, N0.z, N1.z, org.z, iz, t0z, t1z);
+        const float tn = fmaxf(fmaxf(fminf(t0x, t1x), fminf(t0y, t1y)), fminf(t0z, t1z));
+        const float tf = fminf(fminf(fmaxf(t0x, t1x), fmaxf(t0y, t1y)), fmaxf(t0z, t1z));
+        const bool skip = tn > tf || tf < 0.001f || tn > cap;
+        const uint32_t a = __float_as_uint(B0.w);
+        const bool leaf = (a & kLeafBitDev) != 0;
+        const uint32_t child = a + ((oct >> __float_as_uint(B1.w)) & 1u);
+        const uint32_t next = (skip || leaf) ? miss : child;
+        if (!skip && leaf) {
+            const uint32_t first = a & ~kLeafBitDev, count = __float_as_uint(B1.w);
+            tri_done += count;
+            for (uint32_t j = first; j < first + count; ++j)
+                tri_record(p.tbvh_tris + 4u * j, org, dir, best_t, tri_t, tri_i, tri_in);
+            cap = fminf(best_t, tri_t);
+        }
+        node = next;
+    }
+}
+
 // ------------------------------------------------------------ trace kernel
 // kBvh: sphere search through the exact BVH (else brute force).  kLds: the
 // tree is copied into the workgroup's LDS once (persistent grid), so every
@@ -280,13 +425,13 @@ __global__ __launch_bounds__(kLds ? 512 : 256) void trace_kernel(TraceParams p) 
         view = BvhView{p.bvh_nodes, p.bvh_miss, nullptr, p.bvh_prims, p.bvh_prim_id,
                        p.sph_shade, p.sph_kind};
     }
-    const float tmin = 0.001f;                 // common.rs:242, 250
 
     F3 org = f3(0, 0, 0), dir = f3(0, 0, 0);
     float thr_r = 1.0f, thr_g = 1.0f, thr_b = 1.0f;  // ray_color's final_color
     uint32_t rng = 0, slot = 0, bounce = 0;
     bool active = false;
-    uint32_t rays = 0, tri_in = 0, sph_tests = 0, node_tests = 0;
+    uint32_t rays = 0, tri_in = 0, sph_tests = 0, node_tests = 0, tnode_tests = 0,
+             tri_done = 0;
 
     uint32_t pool_next = 0, pool_end = 0;  // wave-uniform job pool
     bool exhausted = false;
@@ -394,22 +539,10 @@ __global__ __launch_bounds__(kLds ? 512 : 256) void trace_kernel(TraceParams p) 
             // Mesh::hit with t_max = best_t, own closest from +inf (common.rs:178-223)
             float tri_t = __builtin_inff();
             int tri_i = -1;
-            for (uint32_t j = 0; j < p.ntri; ++j) {
-                const float4 N = p.tri_hot[j];
-                const float cosl = (N.x * dir.x + N.y * dir.y) + N.z * dir.z;
-                if (-1e-8f < cosl && cosl < 1e-8f) continue;
-                const float t = (((N.x * org.x + N.y * org.y) + N.z * org.z) + N.w) / cosl;
-                if (t < tmin || t > best_t) continue;
-                ++tri_in;
-                const F3 n = f3(N.x, N.y, N.z);
-                const F3 pt = org + scale(dir, t);
-                const float4 *g = p.tri_geo + 4u * j;
-                const float4 A = g[0], B = g[1], Cc = g[2];
-                const F3 v0 = f3(A.x, A.y, A.z), v1 = f3(B.x, B.y, B.z), v2 = f3(Cc.x, Cc.y, Cc.z);
-                if (dot(n, cross(v1 - v0, pt - v0)) < 0.0f) continue;
-                if (dot(n, cross(v2 - v1, pt - v1)) < 0.0f) continue;
-                if (dot(n, cross(v0 - v2, pt - v2)) < 0.0f) continue;
-                if (t < tri_t) { tri_t = t; tri_i = (int)j; }
+            if (p.tnodes != 0) {
+                triangles_bvh(p, org, dir, best_t, tri_t, tri_i, tri_in, tnode_tests, tri_done);
+            } else {
+                triangles_brute(p, org, dir, best_t, tri_t, tri_i, tri_in);
             }
 
             if (tri_i < 0 && best_i < 0) {
@@ -498,14 +631,14 @@ __global__ __launch_bounds__(kLds ? 512 : 256) void trace_kernel(TraceParams p) 
     if (lane == 0)
         for (int k = 0; k < 4; ++k) atomicAdd(&p.stats[4 + k], (unsigned long long)stamp_acc[k]);
 #endif
-    uint64_t c[4] = {rays, tri_in, sph_tests, node_tests};
+    uint64_t c[6] = {rays, tri_in, sph_tests, node_tests, tnode_tests, tri_done};
 #pragma unroll
-    for (int k = 0; k < 4; ++k)
+    for (int k = 0; k < 6; ++k)
         for (uint32_t off = kWave / 2; off > 0; off >>= 1) c[k] += __shfl_xor(c[k], (int)off);
     if (lane == 0) {
 #pragma unroll
-        for (int k = 0; k < 4; ++k)
-            if (c[k]) atomicAdd(&p.stats[k], (unsigned long long)c[k]);
+        for (int k = 0; k < 6; ++k)
+            if (c[k]) atomicAdd(&p.stats[k < 4 ? k : k + 4], (unsigned long long)c[k]);
     }
 }
 

@@ -45,7 +45,7 @@ DeviceState::~DeviceState() {
     if (hipSetDevice(device) != hipSuccess) return;
     void *bufs[] = {sph_hot, sph_cold, tri_hot, tri_geo, mats, samples, out, replay, counter, stats,
                     bvh_nodes, bvh_prims, big_hot, bvh_miss, bvh_prim_id, big_id, bvh_miss16,
-                    sph_shade, sph_kind};
+                    sph_shade, sph_kind, tbvh_nodes, tbvh_tris, tbvh_miss, tbvh_loose};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
     for (hipEvent_t e : ev)
@@ -143,12 +143,27 @@ static int device_for(WorldState &w, int want, DeviceState *&out) {
                 if (d->blocks_per_cu_lds > 0) d->lds_bytes = lds;
             }
         }
+        const TriangleBVH &tb = w.tbvh;
+        if (!tb.nodes.empty()) {
+            auto upu = [&](void **dst, const std::vector<uint32_t> &src) -> hipError_t {
+                hipError_t e = hipMalloc(dst, std::max<size_t>(src.size(), 1) * sizeof(uint32_t));
+                if (e != hipSuccess || src.empty()) return e;
+                return hipMemcpy(*dst, src.data(), src.size() * sizeof(uint32_t), hipMemcpyHostToDevice);
+            };
+            HIP_TRY(up((void **)&d->tbvh_nodes, tb.nodes));
+            HIP_TRY(up((void **)&d->tbvh_tris, tb.tris));
+            HIP_TRY(upu((void **)&d->tbvh_miss, tb.miss));
+            HIP_TRY(upu((void **)&d->tbvh_loose, tb.loose));
+            d->tnodes = (uint32_t)(tb.nodes.size() / 16);
+            d->ttris = (uint32_t)(tb.tris.size() / 16);
+            d->tloose = (uint32_t)tb.loose.size();
+        }
         const uint64_t bpc = env_u64("RT_AMD_BLOCKS_PER_CU", 0);
         if (bpc) d->blocks_per_cu = d->blocks_per_cu_bvh = d->blocks_per_cu_lds = (int)bpc;
         if (d->blocks_per_cu < 1) d->blocks_per_cu = 1;
         if (d->blocks_per_cu_bvh < 1) d->blocks_per_cu_bvh = 1;
         HIP_TRY(hipMalloc((void **)&d->counter, 64));
-        HIP_TRY(hipMalloc((void **)&d->stats, 64));
+        HIP_TRY(hipMalloc((void **)&d->stats, 128));
         slot = std::move(d);
     }
     out = slot.get();
@@ -201,7 +216,7 @@ int render_frame(WorldState &w, const CameraModel &cam, size_t width, size_t hei
         HIP_TRY(grow(d->replay, d->replay_cap, n));
         HIP_TRY(hipMemcpyAsync(d->replay, o.replay_states, n * 4, hipMemcpyHostToDevice, s));
     }
-    HIP_TRY(hipMemsetAsync(d->stats, 0, 64, s));
+    HIP_TRY(hipMemsetAsync(d->stats, 0, 128, s));
 
     TraceParams p{};
     p.sph_hot = d->sph_hot; p.sph_cold = d->sph_cold;
@@ -238,6 +253,15 @@ int render_frame(WorldState &w, const CameraModel &cam, size_t width, size_t hei
         p.use_lds = d->lds_bytes > 0 && env_u64("RT_AMD_LDS", 1) != 0;
         for (int k = 0; k < 3; ++k) p.bvh_c[k] = bv.centre[k];
         p.bvh_r = bv.radius; p.bvh_rmax = bv.rmax; p.bvh_mag = bv.mag;
+    }
+    const bool use_tbvh = d->tnodes > 0 && o.accel != RT_ACCEL_BRUTE;
+    if (use_tbvh) {
+        const TriangleBVH &tb = w.tbvh;
+        p.tbvh_nodes = d->tbvh_nodes; p.tbvh_miss = d->tbvh_miss;
+        p.tbvh_tris = d->tbvh_tris; p.tbvh_loose = d->tbvh_loose;
+        p.tnodes = d->tnodes; p.ttris = d->ttris; p.tloose = d->tloose;
+        for (int k = 0; k < 3; ++k) p.tbvh_c[k] = tb.centre[k];
+        p.tbvh_r = tb.radius; p.tbvh_mag = tb.mag;
     }
     const float inv_spp = 1.0f / (float)o.samples_per_pixel;  // 1.0 / spp as f32 (common.rs:345)
 
@@ -279,24 +303,27 @@ int render_frame(WorldState &w, const CameraModel &cam, size_t width, size_t hei
         trace_ms += a;
         resolve_ms += b;
     }
-    unsigned long long st[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    HIP_TRY(hipMemcpyAsync(st, d->stats, 64, hipMemcpyDeviceToHost, s));
+    unsigned long long st[16] = {};
+    HIP_TRY(hipMemcpyAsync(st, d->stats, 128, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
     if (stats) {
         stats->samples = (uint64_t)T * jobs_per_row;
         stats->rays = st[0];
         stats->sphere_tests = st[0] * (uint64_t)d->nsph;
-        stats->tri_tests = st[0] * (uint64_t)d->ntri;
+        stats->tri_tests = st[0] * (uint64_t)d->ntri;  // the reference's brute-force count
         stats->tri_in_range = st[1];
         stats->trace_ms = trace_ms;
         stats->resolve_ms = resolve_ms;
         stats->trace_launches = launches;
         stats->waves = waves;
-        stats->accel = use_bvh ? RT_ACCEL_BVH : RT_ACCEL_BRUTE;
+        stats->accel = (use_bvh || use_tbvh) ? RT_ACCEL_BVH : RT_ACCEL_BRUTE;
         stats->bvh_sphere_tests = st[2];
         stats->bvh_node_tests = st[3];
         stats->big_sphere_tests = use_bvh ? st[0] * (uint64_t)d->nbig : st[0] * (uint64_t)d->nsph;
         for (int k = 0; k < 4; ++k) stats->stamp_cycles[k] = st[4 + k];
+        stats->tri_node_tests = st[8];
+        stats->tri_bvh = use_tbvh ? 1u : 0u;
+        stats->bvh_tri_tests = use_tbvh ? st[9] : stats->tri_tests;
     }
     return 0;
 }

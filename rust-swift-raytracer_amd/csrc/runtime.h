@@ -35,12 +35,15 @@ struct DeviceState {
     uint32_t *bvh_miss = nullptr, *bvh_prim_id = nullptr, *big_id = nullptr;
     uint16_t *bvh_miss16 = nullptr;
     uint32_t nnodes = 0, nbig = 0, nprims = 0;
+    float4 *tbvh_nodes = nullptr, *tbvh_tris = nullptr;       // triangle BVH (bvh.h)
+    uint32_t *tbvh_miss = nullptr, *tbvh_loose = nullptr;
+    uint32_t tnodes = 0, ttris = 0, tloose = 0;
     size_t lds_bytes = 0;                                       // 0: tree not LDS-stageable
     float4 *samples = nullptr;       size_t samples_cap = 0;   // per-sample colour slab
     uint32_t *out = nullptr;         size_t out_cap = 0;       // RGBA8 tile (host path)
     uint32_t *replay = nullptr;      size_t replay_cap = 0;
     uint32_t *counter = nullptr;                                // job counter
-    unsigned long long *stats = nullptr;                        // [rays, tri_in_range]
+    unsigned long long *stats = nullptr;                        // TraceParams::stats (16 slots)
     int blocks_per_cu = 0, blocks_per_cu_bvh = 0, blocks_per_cu_lds = 0, num_cus = 0;
     size_t last_jobs = 0;                                       // jobs of the last launch
     ~DeviceState();
@@ -50,6 +53,7 @@ struct WorldState {
     SceneModel scene;
     PackedScene packed;
     SphereBVH bvh;
+    TriangleBVH tbvh;
     std::map<int, std::unique_ptr<DeviceState>> devices;
 };
 

@@ -61,7 +61,9 @@ class RenderStats(C.Structure):
                 ("trace_ms", C.c_double), ("resolve_ms", C.c_double),
                 ("trace_launches", C.c_uint32), ("waves", C.c_uint32), ("accel", C.c_uint32),
                 ("bvh_sphere_tests", C.c_uint64), ("bvh_node_tests", C.c_uint64),
-                ("big_sphere_tests", C.c_uint64), ("stamp_cycles", C.c_uint64 * 4)]
+                ("big_sphere_tests", C.c_uint64), ("stamp_cycles", C.c_uint64 * 4),
+                ("tri_node_tests", C.c_uint64), ("bvh_tri_tests", C.c_uint64),
+                ("tri_bvh", C.c_uint32), ("reserved", C.c_uint32)]
 
     def as_dict(self):
         out = {}

@@ -156,9 +156,15 @@ def test_mesh_scene_triangle_path():
                                           record_samples=True)
     world = R.World(src)
     assert world.num_triangles == 100000 and world.num_spheres == 100
-    out, gst = world.render(w, h, spp, 8, mode=R.RNG_COUNTER)
-    assert_bits_equal(out, img, "mesh frame")
+    out, gst = world.render(w, h, spp, 8, mode=R.RNG_COUNTER, accel=R.ACCEL_BRUTE)
+    assert_bits_equal(out, img, "mesh frame (brute force)")
     assert gst["rays"] == st["rays"] and gst["tri_in_range"] == st["tri_in_range"]
+    out, gst = world.render(w, h, spp, 8, mode=R.RNG_COUNTER)
+    assert gst["tri_bvh"] == 1
+    assert_bits_equal(out, img, "mesh frame (BVH)")
+    assert_bits_equal(world.read_samples(w * h * spp)[:, :3],
+                      oracle_samples_to_gpu_order(smp, w, h, spp)[:, :3], "mesh samples")
+    assert gst["rays"] == st["rays"]
 
 
 def test_move_camera_then_render():
@@ -286,6 +292,91 @@ def test_bvh_matches_oracle_rtow():
 def test_bvh_full_size_c2_equals_brute_force():
     """Every pixel and every sample colour of a 1920x1080x16 RTOW frame."""
     a, sa, sma, b, sb, smb = _both_modes(S.rtow(), 1920, 1080, 16)
+    assert_bits_equal(b, a, "frame")
+    assert np.array_equal(smb[:, :3].view(np.uint32), sma[:, :3].view(np.uint32))
+    assert sa["rays"] == sb["rays"]
+
+
+# ------------------------------------------------------- exact triangle BVH
+def _triangle_scene(seed, n, spread=4.0, size=0.5, cam=(0.0, 0.0, 0.0), offset=(0.0, 0.0, 0.0),
+                    slivers=0, dup=0, spheres=0, big=0, grid=0):
+    """Random triangle soup (+ optional spheres) in the scene DSL.  Mixes
+    sizes and orientations, near-degenerate slivers, exact duplicates (equal t:
+    the lower index must win), huge triangles and a coplanar grid."""
+    rng = np.random.default_rng(seed)
+    kinds = ["Diffuse color 0.7 0.5 0.3", "Metal color 0.9 0.8 0.7 fuzz 0.05",
+             "Dielectric ir 1.5", "Metal color 0.6 0.6 0.9 fuzz 0.0"]
+    lines = [f"camera origin {cam[0]:.6f} {cam[1]:.6f} {cam[2]:.6f} aspect 1.5;"]
+    lines += [f"material K{i} : {k};" for i, k in enumerate(kinds)]
+    off = np.array(offset) + np.array([0.0, 0.0, -spread - 2.0])
+    tris = []
+    for _ in range(n):
+        c = rng.uniform(-spread, spread, 3) + off
+        e = rng.normal(size=(2, 3)) * size * rng.uniform(0.1, 1.0)
+        tris.append((c, c + e[0], c + e[1], int(rng.integers(0, 4))))
+    for _ in range(slivers):
+        c = rng.uniform(-spread, spread, 3) + off
+        d = rng.normal(size=3)
+        tris.append((c, c + d, c + 2.0 * d + rng.normal(size=3) * 1e-4, int(rng.integers(0, 4))))
+    for _ in range(big):
+        c = rng.uniform(-spread, spread, 3) + off
+        e = rng.normal(size=(2, 3)) * 40.0
+        tris.append((c, c + e[0], c + e[1], int(rng.integers(0, 4))))
+    for j in range(grid):
+        for i in range(grid):
+            x0, z0 = -3.0 + 6.0 * i / grid, -3.0 + 6.0 * j / grid
+            dx = 6.0 / grid
+            a = np.array([x0, -1.5, z0]) + off
+            b, c2, d = a + [dx, 0, 0], a + [0, 0, dx], a + [dx, 0, dx]
+            tris.append((a, c2, b, 0))
+            tris.append((b, c2, d, 1))
+    tris += tris[:dup]
+    for _ in range(spheres):  # the parser takes spheres before triangles only
+        c = rng.uniform(-spread, spread, 3) + off
+        lines.append(f"sphere center {c[0]:.6f} {c[1]:.6f} {c[2]:.6f} radius "
+                     f"{rng.uniform(0.1, 0.6):.6f} material K{int(rng.integers(0, 4))};")
+    for (v0, v1, v2, k) in tris:
+        lines.append("triangle v0 " + " ".join(f"{x:.6f}" for x in v0) + " v1 " +
+                     " ".join(f"{x:.6f}" for x in v1) + " v2 " +
+                     " ".join(f"{x:.6f}" for x in v2) + f" material K{k};")
+    return "\n".join(lines) + "\n"
+
+
+@pytest.mark.parametrize("case", [
+    dict(seed=11, n=600),
+    dict(seed=12, n=400, size=2.0, dup=80, slivers=30),
+    dict(seed=13, n=300, spheres=200, grid=12),
+    dict(seed=14, n=500, big=6, spread=8.0),
+    dict(seed=15, n=400, offset=(2500.0, -1800.0, 900.0), cam=(2500.0, -1800.0, 900.0)),
+    dict(seed=16, n=400, cam=(0.0, 0.0, -6.0), size=1.0),   # camera inside the soup
+    dict(seed=17, n=200, grid=20, cam=(0.0, 6.0, -4.0)),   # grazing / far phantoms
+])
+def test_triangle_bvh_equals_brute_force(case):
+    src = _triangle_scene(**case)
+    a, sa, sma, b, sb, smb = _both_modes(src, 96, 64, 8)
+    assert sb["tri_bvh"] == 1 and sa["tri_bvh"] == 0
+    assert_bits_equal(b, a, "frame")
+    assert_bits_equal(smb[:, :3], sma[:, :3], "samples")
+    assert sa["rays"] == sb["rays"]
+    assert sb["tri_in_range"] <= sa["tri_in_range"]
+
+
+def test_triangle_bvh_matches_oracle():
+    src = _triangle_scene(21, 300, size=1.0, slivers=10, dup=20, spheres=50)
+    img, st, _, smp = O.Scene(src).render(48, 32, 4, 8, mode=O.RNG_COUNTER, nthreads=8,
+                                          record_samples=True)
+    world = R.World(src)
+    out, gst = world.render(48, 32, 4, 8)
+    assert gst["tri_bvh"] == 1
+    assert_bits_equal(out, img, "frame")
+    assert_bits_equal(world.read_samples(48 * 32 * 4)[:, :3],
+                      oracle_samples_to_gpu_order(smp, 48, 32, 4)[:, :3], "samples")
+
+
+def test_triangle_bvh_c5_equals_brute_force():
+    """Every sample of a 480x270x4 C5 frame (100k triangles + 100 spheres)."""
+    a, sa, sma, b, sb, smb = _both_modes(S.mesh(), 480, 270, 4)
+    assert sb["tri_bvh"] == 1
     assert_bits_equal(b, a, "frame")
     assert np.array_equal(smb[:, :3].view(np.uint32), sma[:, :3].view(np.uint32))
     assert sa["rays"] == sb["rays"]
