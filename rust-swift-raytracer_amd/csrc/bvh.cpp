@@ -207,57 +207,84 @@ static void normal_boxes(const Builder &b, const std::vector<Prim> &prims, uint3
     out[n] = nb;
 }
 
+// Classifies triangle i for the trees: 0 = tree primitive (p filled), 1 =
+// degenerate (never accepted), 2 = brute force (non-finite data, sliver).
+static int triangle_prim(const Triangle &t, const float *h, uint32_t i, Prim &p) {
+    const double v[3][3] = {{t.v0.x, t.v0.y, t.v0.z}, {t.v1.x, t.v1.y, t.v1.z},
+                            {t.v2.x, t.v2.y, t.v2.z}};
+    bool finite = std::isfinite(h[0]) && std::isfinite(h[1]) && std::isfinite(h[2]) &&
+                  std::isfinite(h[3]);
+    for (int k = 0; k < 3; ++k)
+        for (int j = 0; j < 3; ++j) finite = finite && std::isfinite(v[k][j]);
+    const double nn = std::sqrt((double)h[0] * h[0] + (double)h[1] * h[1] + (double)h[2] * h[2]);
+    if (finite && nn == 0.0) return 1;  // cos == 0 for every finite ray: never accepted
+    // The edge tests accept points whose projection along the stored n lies
+    // in the triangle.  Keep only triangles whose stored n is within ~2.6
+    // degrees of the exact plane normal, so that projection is well
+    // conditioned; the rest (slivers, non-finite data) are brute forced.
+    double e1[3], e2[3], tn[3];
+    for (int k = 0; k < 3; ++k) { e1[k] = v[1][k] - v[0][k]; e2[k] = v[2][k] - v[0][k]; }
+    tn[0] = e1[1] * e2[2] - e1[2] * e2[1];
+    tn[1] = e1[2] * e2[0] - e1[0] * e2[2];
+    tn[2] = e1[0] * e2[1] - e1[1] * e2[0];
+    const double tl = std::sqrt(tn[0] * tn[0] + tn[1] * tn[1] + tn[2] * tn[2]);
+    const double cosphi = finite && tl > 0 ? (tn[0] * h[0] + tn[1] * h[1] + tn[2] * h[2]) / (tl * nn)
+                                           : -1.0;
+    if (!(cosphi >= 0.999)) return 2;
+    for (int k = 0; k < 3; ++k) p.n[k] = (double)h[k] / nn;
+    // Accepted points are q + (2 n^.o) n^ + w n^ with q in the triangle and
+    // |w| <= max_i |n^.(v0 - v_i)| (n^ is not exactly normal to the plane).
+    double w = 0;
+    for (int j = 1; j < 3; ++j) {
+        const double d = p.n[0] * (v[0][0] - v[j][0]) + p.n[1] * (v[0][1] - v[j][1]) +
+                         p.n[2] * (v[0][2] - v[j][2]);
+        w = std::max(w, std::fabs(d));
+    }
+    double vm = 0;
+    for (int k = 0; k < 3; ++k)
+        for (int j = 0; j < 3; ++j) vm = std::max(vm, std::fabs(v[k][j]));
+    w = w * (1 + 1e-9) + 1e-15 * vm;
+    for (int k = 0; k < 3; ++k) {
+        const double pad = w * std::fabs(p.n[k]);
+        p.box.lo[k] = std::min({v[0][k], v[1][k], v[2][k]}) - pad;
+        p.box.hi[k] = std::max({v[0][k], v[1][k], v[2][k]}) + pad;
+        p.c[k] = (p.box.lo[k] + p.box.hi[k]) / 2;
+    }
+    p.id = i;
+    return 0;
+}
+
+// 16-float records (n, n.v0) (v0, bits(id)) (v1, 0) (v2, 0) in tree order.
+static std::vector<float> triangle_records(const std::vector<Prim> &prims,
+                                           const std::vector<Triangle> &tris,
+                                           const std::vector<float> &tri_hot) {
+    std::vector<float> out(prims.size() * 16);
+    for (size_t i = 0; i < prims.size(); ++i) {
+        const uint32_t id = prims[i].id;
+        const Triangle &t = tris[id];
+        float *r = &out[i * 16];
+        std::memcpy(r, &tri_hot[(size_t)id * 4], 4 * sizeof(float));
+        const Vec3 vs[3] = {t.v0, t.v1, t.v2};
+        for (int j = 0; j < 3; ++j) {
+            r[4 * (j + 1) + 0] = vs[j].x;
+            r[4 * (j + 1) + 1] = vs[j].y;
+            r[4 * (j + 1) + 2] = vs[j].z;
+            r[4 * (j + 1) + 3] = 0.0f;
+        }
+        r[7] = bits_f(id);
+    }
+    return out;
+}
+
 TriangleBVH build_triangle_bvh(const std::vector<Triangle> &tris, const std::vector<float> &tri_hot,
                                uint32_t leaf_size) {
     TriangleBVH out;
     std::vector<Prim> prims;
     for (uint32_t i = 0; i < tris.size(); ++i) {
-        const Triangle &t = tris[i];
-        const double v[3][3] = {{t.v0.x, t.v0.y, t.v0.z}, {t.v1.x, t.v1.y, t.v1.z},
-                                {t.v2.x, t.v2.y, t.v2.z}};
-        const float *h = &tri_hot[(size_t)i * 4];
-        bool finite = std::isfinite(h[0]) && std::isfinite(h[1]) && std::isfinite(h[2]) &&
-                      std::isfinite(h[3]);
-        for (int k = 0; k < 3; ++k)
-            for (int j = 0; j < 3; ++j) finite = finite && std::isfinite(v[k][j]);
-        const double nn = std::sqrt((double)h[0] * h[0] + (double)h[1] * h[1] + (double)h[2] * h[2]);
-        if (finite && nn == 0.0) continue;  // cos == 0 for every finite ray: never accepted
-        // The edge tests accept points whose projection along the stored n lies
-        // in the triangle.  Keep only triangles whose stored n is within ~2.6
-        // degrees of the exact plane normal, so that projection is well
-        // conditioned; the rest (slivers, non-finite data) are brute forced.
-        double e1[3], e2[3], tn[3];
-        for (int k = 0; k < 3; ++k) { e1[k] = v[1][k] - v[0][k]; e2[k] = v[2][k] - v[0][k]; }
-        tn[0] = e1[1] * e2[2] - e1[2] * e2[1];
-        tn[1] = e1[2] * e2[0] - e1[0] * e2[2];
-        tn[2] = e1[0] * e2[1] - e1[1] * e2[0];
-        const double tl = std::sqrt(tn[0] * tn[0] + tn[1] * tn[1] + tn[2] * tn[2]);
-        const double cosphi = finite && tl > 0
-                                  ? (tn[0] * h[0] + tn[1] * h[1] + tn[2] * h[2]) / (tl * nn)
-                                  : -1.0;
-        if (!(cosphi >= 0.999)) { out.loose.push_back(i); continue; }
         Prim p;
-        for (int k = 0; k < 3; ++k) p.n[k] = (double)h[k] / nn;
-        // Accepted points are q + (2 n^.o) n^ + w n^ with q in the triangle and
-        // |w| <= max_i |n^.(v0 - v_i)| (n^ is not exactly normal to the plane).
-        double w = 0;
-        for (int j = 1; j < 3; ++j) {
-            const double d = p.n[0] * (v[0][0] - v[j][0]) + p.n[1] * (v[0][1] - v[j][1]) +
-                             p.n[2] * (v[0][2] - v[j][2]);
-            w = std::max(w, std::fabs(d));
-        }
-        double vm = 0;
-        for (int k = 0; k < 3; ++k)
-            for (int j = 0; j < 3; ++j) vm = std::max(vm, std::fabs(v[k][j]));
-        w = w * (1 + 1e-9) + 1e-15 * vm;
-        for (int k = 0; k < 3; ++k) {
-            const double pad = w * std::fabs(p.n[k]);
-            p.box.lo[k] = std::min({v[0][k], v[1][k], v[2][k]}) - pad;
-            p.box.hi[k] = std::max({v[0][k], v[1][k], v[2][k]}) + pad;
-            p.c[k] = (p.box.lo[k] + p.box.hi[k]) / 2;
-        }
-        p.id = i;
-        prims.push_back(p);
+        const int kind = triangle_prim(tris[i], &tri_hot[(size_t)i * 4], i, p);
+        if (kind == 0) prims.push_back(p);
+        else if (kind == 2) out.loose.push_back(i);
     }
     if (prims.size() < 16) {  // not worth a tree: brute force keeps the reference order
         out.loose.clear();
@@ -311,21 +338,53 @@ TriangleBVH build_triangle_bvh(const std::vector<Triangle> &tris, const std::vec
     }
     out.miss.assign(b.nodes.size() * 8, kNodeEnd);
     for (uint32_t oct = 0; oct < 8; ++oct) b.links(0, kNodeEnd, oct, out.miss);
-    out.tris.resize(prims.size() * 16);
-    for (size_t i = 0; i < prims.size(); ++i) {
-        const uint32_t id = prims[i].id;
-        const Triangle &t = tris[id];
-        float *r = &out.tris[i * 16];
-        std::memcpy(r, &tri_hot[(size_t)id * 4], 4 * sizeof(float));
-        const Vec3 vs[3] = {t.v0, t.v1, t.v2};
-        for (int j = 0; j < 3; ++j) {
-            r[4 * (j + 1) + 0] = vs[j].x;
-            r[4 * (j + 1) + 1] = vs[j].y;
-            r[4 * (j + 1) + 2] = vs[j].z;
-            r[4 * (j + 1) + 3] = 0.0f;
+    out.tris = triangle_records(prims, tris, tri_hot);
+    return out;
+}
+
+CameraTriangleBVH build_camera_triangle_bvh(const std::vector<Triangle> &tris,
+                                            const std::vector<float> &tri_hot, const TriangleBVH &tb,
+                                            const float origin[3], uint32_t leaf_size) {
+    CameraTriangleBVH out;
+    for (int k = 0; k < 3; ++k) out.origin[k] = origin[k];
+    if (tb.nodes.empty()) return out;
+    const double o[3] = {origin[0], origin[1], origin[2]};
+    const double onorm = std::fabs(o[0]) + std::fabs(o[1]) + std::fabs(o[2]);
+    if (!(onorm < 1e18)) return out;  // the kernel brute-forces such origins
+    // the kernel's per-ray margin (render.hip triangles_bvh) for this origin
+    double dist = tb.radius + 2 * onorm;
+    for (int k = 0; k < 3; ++k) dist += std::fabs(o[k] - tb.centre[k]);
+    const double rho = 1e-5 * (dist + onorm + tb.mag) * (1 + 1e-6);
+    std::vector<Prim> prims;
+    for (uint32_t i = 0; i < tris.size(); ++i) {
+        Prim p;
+        if (triangle_prim(tris[i], &tri_hot[(size_t)i * 4], i, p) != 0) continue;
+        const double sdot = p.n[0] * o[0] + p.n[1] * o[1] + p.n[2] * o[2];
+        for (int k = 0; k < 3; ++k) {
+            const double off = 2 * sdot * p.n[k];
+            p.box.lo[k] += off - rho;
+            p.box.hi[k] += off + rho;
+            p.c[k] = (p.box.lo[k] + p.box.hi[k]) / 2;
         }
-        r[7] = bits_f(id);
+        prims.push_back(p);
     }
+    if (prims.empty()) return out;
+    Builder b(prims, std::max(1u, leaf_size));
+    b.nodes.reserve(prims.size() * 2);
+    b.nodes.emplace_back();
+    b.build(0, 0, (uint32_t)prims.size(), 0);
+    out.depth = b.max_depth;
+    out.nodes.resize(b.nodes.size() * 8);
+    for (size_t n = 0; n < b.nodes.size(); ++n) {
+        const auto &nd = b.nodes[n];
+        float *f = &out.nodes[n * 8];
+        for (int k = 0; k < 3; ++k) { f[k] = down(nd.box.lo[k]); f[4 + k] = up(nd.box.hi[k]); }
+        f[3] = bits_f(nd.leaf ? (nd.a | kLeafBit) : nd.a);
+        f[7] = bits_f(nd.b);
+    }
+    out.miss.assign(b.nodes.size() * 8, kNodeEnd);
+    for (uint32_t oct = 0; oct < 8; ++oct) b.links(0, kNodeEnd, oct, out.miss);
+    out.tris = triangle_records(prims, tris, tri_hot);
     return out;
 }
 

@@ -64,4 +64,21 @@ struct TriangleBVH {
 TriangleBVH build_triangle_bvh(const std::vector<Triangle> &tris, const std::vector<float> &tri_hot,
                                uint32_t leaf_size);
 
+// Primary rays all start at the camera origin, so their phantom triangles are
+// fixed: this tree holds, per triangle of `tb`, its box translated by
+// 2(n^.o)n^ for o = origin and padded by the kernel's margin rho(o), under a
+// plain SAH build.  Bounce-0 rays traverse it with an ordinary slab test.
+// Nodes as SphereBVH (8 floats); tris/miss as TriangleBVH.  Rebuilt whenever
+// the camera moves (load_world, move_camera_position).
+struct CameraTriangleBVH {
+    std::vector<float> nodes;
+    std::vector<uint32_t> miss;
+    std::vector<float> tris;
+    float origin[3] = {0, 0, 0};
+    uint32_t depth = 0;
+};
+CameraTriangleBVH build_camera_triangle_bvh(const std::vector<Triangle> &tris,
+                                            const std::vector<float> &tri_hot, const TriangleBVH &tb,
+                                            const float origin[3], uint32_t leaf_size);
+
 }  // namespace rtamd

@@ -56,6 +56,9 @@ Rust_WorldHandle *load_world(const char *source) {
     world->state.tbvh = rtamd::build_triangle_bvh(world->state.scene.triangles,
                                                   world->state.packed.tri_hot,
                                                   tleaf ? (uint32_t)std::atoi(tleaf) : 4u);
+    // bounce-0 triangle tree for the scene camera (rebuilt by the first render
+    // after move_camera_position, which does not see the world)
+    rtamd::prepare_camera(world->state, world->state.scene.camera);
     auto *cam = new Rust_Camera{world->state.scene.camera};
     return new Rust_WorldHandle{world, cam};
 }

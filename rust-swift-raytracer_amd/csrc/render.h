@@ -58,6 +58,12 @@ struct TraceParams {
     const uint32_t *tbvh_loose;  // triangles tested by brute force, ascending
     uint32_t tnodes, ttris, tloose;
     float tbvh_c[3], tbvh_r, tbvh_mag;
+    // the same triangles' phantoms for the camera origin (bvh.h CameraTriangleBVH),
+    // used at bounce 0; cam_nnodes == 0: bounce 0 uses the tree above
+    const float4 *cam_nodes;  // 2 per node
+    const uint32_t *cam_miss; // 8 per node
+    const float4 *cam_tris;   // 4 per triangle, as tbvh_tris
+    uint32_t cam_nnodes;
 };
 
 hipError_t launch_trace(const TraceParams &p, uint32_t blocks, hipStream_t stream);

@@ -312,8 +312,13 @@ __device__ __forceinline__ bool tri_record(const float4 *r, F3 org, F3 dir, floa
 // box) plus rho, a rounding margin that dominates every error term
 // (<= ~40u (dist + |o| + M)), and skips only nodes the ray
 // certainly misses or enters beyond min(best_t, tri_t).
+//
+// cam (bounce 0, org == camera origin): the lane walks the camera-origin tree
+// instead, whose boxes already are the phantoms of that origin padded by rho
+// (bvh.h CameraTriangleBVH) -- same loop, no widening, so lanes at bounce 0
+// and lanes further down their paths do not serialise.
 __device__ __forceinline__ void triangles_bvh(const TraceParams &p, F3 org, F3 dir, float best_t,
-                                              float &tri_t, int &tri_i, uint32_t &tri_in,
+                                              bool cam, float &tri_t, int &tri_i, uint32_t &tri_in,
                                               uint32_t &node_tests, uint32_t &tri_done) {
     tri_done += p.tloose;
     for (uint32_t k = 0; k < p.tloose; ++k) {  // slivers / non-finite data
@@ -329,7 +334,7 @@ __device__ __forceinline__ void triangles_bvh(const TraceParams &p, F3 org, F3 d
             tri_merge(t, (int)j, tri_t, tri_i);
     }
     const float onorm = (fabsf(org.x) + fabsf(org.y)) + fabsf(org.z);
-    if (!(onorm < 1e18f)) {
+    if (!cam && !(onorm < 1e18f)) {
         // far / non-finite origin: the margins below would overflow; every
         // record is tested instead (order-independent merge, same result)
         tri_done += p.ttris;
@@ -342,14 +347,20 @@ __device__ __forceinline__ void triangles_bvh(const TraceParams &p, F3 org, F3 d
     // distance from o to any phantom point: |o - c| + radius + 2|o|
     const float dist = ((fabsf(org.x - p.tbvh_c[0]) + fabsf(org.y - p.tbvh_c[1])) +
                         fabsf(org.z - p.tbvh_c[2])) + p.tbvh_r + 2.0f * onorm;
-    const float rho = 1e-5f * ((dist + onorm) + p.tbvh_mag);
+    const float rho = cam ? 0.0f : 1e-5f * ((dist + onorm) + p.tbvh_mag);
+    const float4 *nodes = cam ? p.cam_nodes : p.tbvh_nodes;
+    const uint32_t *links = cam ? p.cam_miss : p.tbvh_miss;
+    const float4 *recs = cam ? p.cam_tris : p.tbvh_tris;
+    const uint32_t stride = cam ? 2u : 4u;
     float cap = fminf(best_t, tri_t);
     uint32_t node = 0;
     while (node != kNodeEndDev) {
         ++node_tests;
-        const float4 *nd = p.tbvh_nodes + 4u * node;
-        const float4 B0 = nd[0], B1 = nd[1], N0 = nd[2], N1 = nd[3];
-        const uint32_t miss = p.tbvh_miss[8u * node + oct];
+        const float4 *nd = nodes + stride * node;
+        const float4 B0 = nd[0], B1 = nd[1];
+        float4 N0 = make_float4(0.0f, 0.0f, 0.0f, 0.0f), N1 = N0;  // camera tree: no widening
+        if (!cam) { N0 = nd[2]; N1 = nd[3]; }
+        const uint32_t miss = links[8u * node + oct];
         // s = n^.o over the normal box
         const float ax = N0.x * org.x, bx = N1.x * org.x;
         const float ay = N0.y * org.y, by = N1.y * org.y;
@@ -382,7 +393,7 @@ __device__ __forceinline__ void triangles_bvh(const TraceParams &p, F3 org, F3 d
             const uint32_t first = a & ~kLeafBitDev, count = __float_as_uint(B1.w);
             tri_done += count;
             for (uint32_t j = first; j < first + count; ++j)
-                tri_record(p.tbvh_tris + 4u * j, org, dir, best_t, tri_t, tri_i, tri_in);
+                tri_record(recs + 4u * j, org, dir, best_t, tri_t, tri_i, tri_in);
             cap = fminf(best_t, tri_t);
         }
         node = next;
@@ -540,7 +551,8 @@ __global__ __launch_bounds__(kLds ? 512 : 256) void trace_kernel(TraceParams p) 
             float tri_t = __builtin_inff();
             int tri_i = -1;
             if (p.tnodes != 0) {
-                triangles_bvh(p, org, dir, best_t, tri_t, tri_i, tri_in, tnode_tests, tri_done);
+                triangles_bvh(p, org, dir, best_t, bounce == 0 && p.cam_nnodes != 0, tri_t, tri_i,
+                              tri_in, tnode_tests, tri_done);
             } else {
                 triangles_brute(p, org, dir, best_t, tri_t, tri_i, tri_in);
             }

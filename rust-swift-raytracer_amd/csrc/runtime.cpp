@@ -45,7 +45,8 @@ DeviceState::~DeviceState() {
     if (hipSetDevice(device) != hipSuccess) return;
     void *bufs[] = {sph_hot, sph_cold, tri_hot, tri_geo, mats, samples, out, replay, counter, stats,
                     bvh_nodes, bvh_prims, big_hot, bvh_miss, bvh_prim_id, big_id, bvh_miss16,
-                    sph_shade, sph_kind, tbvh_nodes, tbvh_tris, tbvh_miss, tbvh_loose};
+                    sph_shade, sph_kind, tbvh_nodes, tbvh_tris, tbvh_miss, tbvh_loose,
+                    cam_nodes, cam_tris, cam_miss};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
     for (hipEvent_t e : ev)
@@ -170,6 +171,16 @@ static int device_for(WorldState &w, int want, DeviceState *&out) {
     return 0;
 }
 
+void prepare_camera(WorldState &w, const CameraModel &cam) {
+    if (w.tbvh.nodes.empty() || env_u64("RT_AMD_CAMERA_TREE", 1) == 0) return;
+    const float o[3] = {cam.origin.x, cam.origin.y, cam.origin.z};
+    if (w.ctree_version && std::memcmp(o, w.ctree.origin, sizeof(o)) == 0) return;
+    const uint64_t leaf = env_u64("RT_AMD_TRI_LEAF", 4);
+    w.ctree = build_camera_triangle_bvh(w.scene.triangles, w.packed.tri_hot, w.tbvh, o,
+                                        (uint32_t)leaf);
+    ++w.ctree_version;
+}
+
 template <typename T>
 static hipError_t grow(T *&buf, size_t &cap, size_t n) {
     if (n <= cap) return hipSuccess;
@@ -255,7 +266,30 @@ int render_frame(WorldState &w, const CameraModel &cam, size_t width, size_t hei
         p.bvh_r = bv.radius; p.bvh_rmax = bv.rmax; p.bvh_mag = bv.mag;
     }
     const bool use_tbvh = d->tnodes > 0 && o.accel != RT_ACCEL_BRUTE;
+    if (use_tbvh) prepare_camera(w, cam);
+    if (use_tbvh && w.ctree_version && d->cam_version != w.ctree_version) {
+        for (void *b : {(void *)d->cam_nodes, (void *)d->cam_tris, (void *)d->cam_miss})
+            if (b) HIP_TRY(hipFree(b));
+        d->cam_nodes = d->cam_tris = nullptr;
+        d->cam_miss = nullptr;
+        d->cam_nnodes = 0;
+        const CameraTriangleBVH &ct = w.ctree;
+        if (!ct.nodes.empty()) {
+            HIP_TRY(hipMalloc((void **)&d->cam_nodes, ct.nodes.size() * 4));
+            HIP_TRY(hipMemcpy(d->cam_nodes, ct.nodes.data(), ct.nodes.size() * 4, hipMemcpyHostToDevice));
+            HIP_TRY(hipMalloc((void **)&d->cam_tris, ct.tris.size() * 4));
+            HIP_TRY(hipMemcpy(d->cam_tris, ct.tris.data(), ct.tris.size() * 4, hipMemcpyHostToDevice));
+            HIP_TRY(hipMalloc((void **)&d->cam_miss, ct.miss.size() * 4));
+            HIP_TRY(hipMemcpy(d->cam_miss, ct.miss.data(), ct.miss.size() * 4, hipMemcpyHostToDevice));
+            d->cam_nnodes = (uint32_t)(ct.nodes.size() / 8);
+        }
+        d->cam_version = w.ctree_version;
+    }
     if (use_tbvh) {
+        if (d->cam_nnodes && std::memcmp(w.ctree.origin, &cam.origin, 12) == 0) {
+            p.cam_nodes = d->cam_nodes; p.cam_miss = d->cam_miss; p.cam_tris = d->cam_tris;
+            p.cam_nnodes = d->cam_nnodes;
+        }
         const TriangleBVH &tb = w.tbvh;
         p.tbvh_nodes = d->tbvh_nodes; p.tbvh_miss = d->tbvh_miss;
         p.tbvh_tris = d->tbvh_tris; p.tbvh_loose = d->tbvh_loose;

@@ -38,6 +38,10 @@ struct DeviceState {
     float4 *tbvh_nodes = nullptr, *tbvh_tris = nullptr;       // triangle BVH (bvh.h)
     uint32_t *tbvh_miss = nullptr, *tbvh_loose = nullptr;
     uint32_t tnodes = 0, ttris = 0, tloose = 0;
+    float4 *cam_nodes = nullptr, *cam_tris = nullptr;         // camera-origin triangle BVH
+    uint32_t *cam_miss = nullptr;
+    uint32_t cam_nnodes = 0;
+    uint64_t cam_version = 0;                                  // WorldState::ctree_version uploaded
     size_t lds_bytes = 0;                                       // 0: tree not LDS-stageable
     float4 *samples = nullptr;       size_t samples_cap = 0;   // per-sample colour slab
     uint32_t *out = nullptr;         size_t out_cap = 0;       // RGBA8 tile (host path)
@@ -54,6 +58,8 @@ struct WorldState {
     PackedScene packed;
     SphereBVH bvh;
     TriangleBVH tbvh;
+    CameraTriangleBVH ctree;      // for the camera origin of ctree_version
+    uint64_t ctree_version = 0;   // 0: none built
     std::map<int, std::unique_ptr<DeviceState>> devices;
 };
 
@@ -66,6 +72,10 @@ int render_frame(WorldState &w, const CameraModel &cam, size_t width, size_t hei
 // Same, into host memory (the reference's synchronous render(), lib.rs:49-57).
 int render_frame_host(WorldState &w, const CameraModel &cam, size_t width, size_t height,
                       const RtRenderOptions &opts, void *host_out, RtRenderStats *stats);
+
+// (Re)builds the camera-origin triangle tree when the origin changed
+// (load_world, move_camera_position, or a render with another camera).
+void prepare_camera(WorldState &w, const CameraModel &cam);
 
 long read_samples(WorldState &w, int device, float *out, size_t n);
 

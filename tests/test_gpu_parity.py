@@ -380,3 +380,19 @@ def test_triangle_bvh_c5_equals_brute_force():
     assert_bits_equal(b, a, "frame")
     assert np.array_equal(smb[:, :3].view(np.uint32), sma[:, :3].view(np.uint32))
     assert sa["rays"] == sb["rays"]
+
+
+def test_triangle_camera_tree_follows_camera_moves():
+    """Bounce-0 rays use a tree built for the camera origin; moving the camera
+    must rebuild it (every sample still equals brute force)."""
+    src = _triangle_scene(31, 500, size=1.0, spheres=30, grid=10)
+    world = R.World(src)
+    for mv in [(0.0, 0.0, 0.0), (0.5, -0.25, 1.0), (-3.0, 2.0, -4.0), (0.0, 0.0, 0.0)]:
+        world.move_camera(*mv)
+        a, sa = world.render(64, 48, 4, 8, accel=R.ACCEL_BRUTE)
+        sma = world.read_samples(64 * 48 * 4)
+        b, sb = world.render(64, 48, 4, 8, accel=R.ACCEL_BVH)
+        smb = world.read_samples(64 * 48 * 4)
+        assert sb["tri_bvh"] == 1
+        assert_bits_equal(b, a, f"frame after move {mv}")
+        assert_bits_equal(smb[:, :3], sma[:, :3], f"samples after move {mv}")
