@@ -61,8 +61,8 @@ typedef struct RtRenderStats {
   uint64_t bvh_node_tests;   /* BVH node (box) tests executed                */
   uint64_t big_sphere_tests; /* rays * spheres kept out of the BVH           */
   uint64_t stamp_cycles[4];  /* diagnostic builds (-DRT_STAMPS) only: wave
-                                cycles in refill / sphere search / shading /
-                                store; zero in the product build             */
+                                cycles in refill+store / ray setup / BVH
+                                walks / shading; zero in the product build             */
   uint64_t tri_node_tests;   /* triangle-BVH node tests executed              */
   uint64_t bvh_tri_tests;    /* triangle tests executed (== tri_tests brute)  */
   uint32_t tri_bvh;          /* 1 when the triangle BVH ran                   */

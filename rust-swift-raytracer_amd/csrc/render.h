@@ -50,6 +50,8 @@ struct TraceParams {
     const uint32_t *sph_kind; // material kind per sphere
     FastDiv div_npix, div_width, div_rowblock;  // job -> (sample, pixel) mapping
     uint32_t refill_min;      // refill dead lanes once at least this many are idle
+    uint32_t steps;           // BVH nodes a lane walks per loop iteration (>= 1) ...
+    uint32_t step;            // ... when nonzero (else walks run to the end)
     float bvh_c[3], bvh_r, bvh_rmax, bvh_mag;
     // phantom-aware triangle BVH (bvh.h TriangleBVH); tnodes == 0: brute-force Mesh loop
     const float4 *tbvh_nodes; // 4 per node: (min, a) (max, b) (normal min) (normal max)
@@ -71,8 +73,9 @@ hipError_t launch_trace(const TraceParams &p, uint32_t blocks, hipStream_t strea
 hipError_t launch_resolve_ex(const float4 *samples, uint32_t *out, uint32_t npix, uint32_t spp,
                              float inv_spp, uint32_t width, uint32_t slab_row0,
                              hipStream_t stream);
-// variant: 0 brute force, 1 BVH from global memory, 2 BVH staged in LDS
-hipError_t trace_occupancy(int *blocks_per_cu, int variant, size_t lds_bytes);
+// variant: 0 brute force, 1 BVH from global memory, 2 BVH staged in LDS;
+// step: the sliced-walk kernel (TraceParams::step)
+hipError_t trace_occupancy(int *blocks_per_cu, int variant, size_t lds_bytes, bool step);
 size_t trace_lds_bytes(const TraceParams &p);
 
 }  // namespace rtamd

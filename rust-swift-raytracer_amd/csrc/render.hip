@@ -177,71 +177,75 @@ struct BvhView {
     const uint32_t *kinds;
 };
 
-// Spheres through the exact-pruning BVH (bvh.h).  Big spheres first (brute
-// force, wave-uniform), then a stackless octant-ordered traversal: every
-// node box is inflated per ray by e = K*(min(A, best_t + R)*(1+3K) + R) + e_abs,
-// which bounds how far a computed candidate's point can lie outside its
-// sphere; a node is skipped only when the inflated box is certainly missed
-// or certainly starts beyond best_t.
-template <bool kLds>
-__device__ __forceinline__ void spheres_bvh(const TraceParams &p, const BvhView &v, F3 org, F3 dir,
-                                            float &best_t, int &best_i, uint32_t &sph_tests,
-                                            uint32_t &node_tests) {
+// Spheres through the exact-pruning BVH (bvh.h): big spheres first (brute
+// force, wave-uniform), then a stackless octant-ordered traversal that the
+// kernel advances a bounded number of nodes per loop iteration (sphere_step),
+// so a lane whose search ends early picks up new work instead of idling
+// behind the wave's longest search.  Every node box is inflated per ray by
+// e = K*(min(A, best_t + R)*(1+3K) + R) + e_abs, which bounds how far a
+// computed candidate's point can lie outside its sphere; a node is skipped
+// only when the inflated box is certainly missed or certainly starts beyond
+// best_t.
+struct SphBound { float A, e_abs; };  // per-ray inputs of the inflation
+__device__ __forceinline__ SphBound sph_bound(const TraceParams &p, F3 org) {
+    const float ax = org.x - p.bvh_c[0], ay = org.y - p.bvh_c[1], az = org.z - p.bvh_c[2];
+    return SphBound{__builtin_sqrtf((ax * ax + ay * ay) + az * az) * 1.00001f + p.bvh_r,
+                    2e-6f * ((fabsf(org.x) + fabsf(org.y)) + fabsf(org.z) + p.bvh_mag)};
+}
+__device__ __forceinline__ float sph_inflation(const TraceParams &p, SphBound b, float bt) {
+    const float a = fminf(b.A, bt + p.bvh_rmax);  // fminf(A, inf) = A
+    return kErrK * (a * (1.0f + 3.0f * kErrK) + p.bvh_rmax) + b.e_abs;
+}
+
+__device__ __forceinline__ void spheres_big(const TraceParams &p, F3 org, F3 dir, float &best_t,
+                                            int &best_i) {
     for (uint32_t k = 0; k < p.nbig; ++k) {
         const float4 S = uniform_load(p.big_hot, k);
-        const int idx = (int)p.big_id[k];
-        sphere_candidate(S, org, dir, idx, best_t, best_i);
+        sphere_candidate(S, org, dir, (int)p.big_id[k], best_t, best_i);
     }
-    if (p.ablate & 1u) return;  // timing-only diagnostic build path: results are wrong
-    const float ix = 1.0f / dir.x, iy = 1.0f / dir.y, iz = 1.0f / dir.z;
-    const uint32_t oct = (ix < 0.0f ? 1u : 0u) | (iy < 0.0f ? 2u : 0u) | (iz < 0.0f ? 4u : 0u);
-    const float ax = org.x - p.bvh_c[0], ay = org.y - p.bvh_c[1], az = org.z - p.bvh_c[2];
-    const float A = __builtin_sqrtf((ax * ax + ay * ay) + az * az) * 1.00001f + p.bvh_r;
-    const float e_abs = 2e-6f * ((fabsf(org.x) + fabsf(org.y)) + fabsf(org.z) + p.bvh_mag);
-    auto inflation = [&](float bt) {
-        const float a = fminf(A, bt + p.bvh_rmax);  // fminf(A, inf) = A
-        return kErrK * (a * (1.0f + 3.0f * kErrK) + p.bvh_rmax) + e_abs;
-    };
-    float e = inflation(best_t);
-    F3 lo = f3(org.x + e, org.y + e, org.z + e);  // (bmin - e) - o == bmin - (o + e)
-    F3 hi = f3(org.x - e, org.y - e, org.z - e);
-    const uint32_t kEnd = kLds ? 0xFFFFu : kNodeEndDev;
-    uint32_t node = 0;
-    while (node != kEnd) {
-        ++node_tests;
-        const float4 B0 = v.nodes[2 * node];
-        const float4 B1 = v.nodes[2 * node + 1];
-        const uint32_t miss = kLds ? (uint32_t)v.miss16[8 * node + oct] : v.miss32[8 * node + oct];
-        // Each computed slab value is (b - lo)(1+d1) * inv(1+d2)(1+d3): the
-        // exact value for a face moved by <= 3u|b - lo|, which e_abs covers,
-        // so [tn, tf] is the exact interval of a box that still contains
-        // every inflated sphere of the node: plain comparisons are safe.
-        const float t0x = (B0.x - lo.x) * ix, t1x = (B1.x - hi.x) * ix;
-        const float t0y = (B0.y - lo.y) * iy, t1y = (B1.y - hi.y) * iy;
-        const float t0z = (B0.z - lo.z) * iz, t1z = (B1.z - hi.z) * iz;
-        const float tn = fmaxf(fmaxf(fminf(t0x, t1x), fminf(t0y, t1y)), fminf(t0z, t1z));
-        const float tf = fminf(fminf(fmaxf(t0x, t1x), fmaxf(t0y, t1y)), fmaxf(t0z, t1z));
-        // NaN (0 * inf on a degenerate slab) compares false: never a skip
-        const bool skip = tn > tf || tf < 0.001f || tn > best_t;
-        const uint32_t a = __float_as_uint(B0.w);
-        const bool leaf = (a & kLeafBitDev) != 0;
-        const uint32_t child = a + ((oct >> __float_as_uint(B1.w)) & 1u);  // near child first
-        const uint32_t next = (skip || leaf) ? miss : child;
-        if (!skip && leaf) {
-            const uint32_t first = a & ~kLeafBitDev, count = __float_as_uint(B1.w);
-            bool changed = false;
-            for (uint32_t j = first; j < first + count; ++j) {
-                ++sph_tests;
-                changed |= sphere_candidate(v.prims[j], org, dir, (int)v.ids[j], best_t, best_i);
-            }
-            if (changed) {
-                e = inflation(best_t);
-                lo = f3(org.x + e, org.y + e, org.z + e);
-                hi = f3(org.x - e, org.y - e, org.z - e);
-            }
+}
+
+// One node of the sphere tree.  node becomes the end marker when the search
+// is over: kNodeEndDev, or 0xFFFF for the LDS copy's u16 links.
+template <bool kLds>
+__device__ __forceinline__ void sphere_step(const TraceParams &p, const BvhView &v, F3 org, F3 dir,
+                                            F3 inv, uint32_t oct, uint32_t &node, float &best_t,
+                                            int &best_i, SphBound bnd, F3 &lo, F3 &hi,
+                                            uint32_t &sph_tests, uint32_t &node_tests) {
+    ++node_tests;
+    const float4 B0 = v.nodes[2 * node];
+    const float4 B1 = v.nodes[2 * node + 1];
+    const uint32_t miss = kLds ? (uint32_t)v.miss16[8 * node + oct] : v.miss32[8 * node + oct];
+    // Each computed slab value is (b - lo)(1+d1) * inv(1+d2)(1+d3): the exact
+    // value for a face moved by <= 3u|b - lo|, which e_abs covers, so
+    // [tn, tf] is the exact interval of a box that still contains every
+    // inflated sphere of the node: plain comparisons are safe.
+    // lo = o + e, hi = o - e:  (bmin - e) - o == bmin - (o + e)
+    const float t0x = (B0.x - lo.x) * inv.x, t1x = (B1.x - hi.x) * inv.x;
+    const float t0y = (B0.y - lo.y) * inv.y, t1y = (B1.y - hi.y) * inv.y;
+    const float t0z = (B0.z - lo.z) * inv.z, t1z = (B1.z - hi.z) * inv.z;
+    const float tn = fmaxf(fmaxf(fminf(t0x, t1x), fminf(t0y, t1y)), fminf(t0z, t1z));
+    const float tf = fminf(fminf(fmaxf(t0x, t1x), fmaxf(t0y, t1y)), fmaxf(t0z, t1z));
+    // NaN (0 * inf on a degenerate slab) compares false: never a skip
+    const bool skip = tn > tf || tf < 0.001f || tn > best_t;
+    const uint32_t a = __float_as_uint(B0.w);
+    const bool leaf = (a & kLeafBitDev) != 0;
+    const uint32_t child = a + ((oct >> __float_as_uint(B1.w)) & 1u);  // near child first
+    const uint32_t next = (skip || leaf) ? miss : child;
+    if (!skip && leaf) {
+        const uint32_t first = a & ~kLeafBitDev, count = __float_as_uint(B1.w);
+        bool changed = false;
+        for (uint32_t j = first; j < first + count; ++j) {
+            ++sph_tests;
+            changed |= sphere_candidate(v.prims[j], org, dir, (int)v.ids[j], best_t, best_i);
         }
-        node = next;
+        if (changed) {
+            const float e = sph_inflation(p, bnd, best_t);
+            lo = f3(org.x + e, org.y + e, org.z + e);
+            hi = f3(org.x - e, org.y - e, org.z - e);
+        }
     }
+    node = next;
 }
 
 // ------------------------------------------------------------ triangle stage
@@ -315,11 +319,16 @@ __device__ __forceinline__ bool tri_record(const float4 *r, F3 org, F3 dir, floa
 //
 // cam (bounce 0, org == camera origin): the lane walks the camera-origin tree
 // instead, whose boxes already are the phantoms of that origin padded by rho
-// (bvh.h CameraTriangleBVH) -- same loop, no widening, so lanes at bounce 0
+// (bvh.h CameraTriangleBVH) -- same step, no widening, so lanes at bounce 0
 // and lanes further down their paths do not serialise.
-__device__ __forceinline__ void triangles_bvh(const TraceParams &p, F3 org, F3 dir, float best_t,
-                                              bool cam, float &tri_t, int &tri_i, uint32_t &tri_in,
-                                              uint32_t &node_tests, uint32_t &tri_done) {
+//
+// tri_begin: brute-forced triangles, then the walk's margin.  Returns false
+// when the walk is not needed (far / non-finite origin: every record is tested
+// here instead -- the margins would overflow; same result by the
+// order-independent merge).
+__device__ __forceinline__ bool tri_begin(const TraceParams &p, F3 org, F3 dir, float best_t,
+                                          bool cam, float &rho, float &tri_t, int &tri_i,
+                                          uint32_t &tri_in, uint32_t &tri_done) {
     tri_done += p.tloose;
     for (uint32_t k = 0; k < p.tloose; ++k) {  // slivers / non-finite data
         const uint32_t j = p.tbvh_loose[k];
@@ -335,76 +344,76 @@ __device__ __forceinline__ void triangles_bvh(const TraceParams &p, F3 org, F3 d
     }
     const float onorm = (fabsf(org.x) + fabsf(org.y)) + fabsf(org.z);
     if (!cam && !(onorm < 1e18f)) {
-        // far / non-finite origin: the margins below would overflow; every
-        // record is tested instead (order-independent merge, same result)
         tri_done += p.ttris;
         for (uint32_t j = 0; j < p.ttris; ++j)
             tri_record(p.tbvh_tris + 4u * j, org, dir, best_t, tri_t, tri_i, tri_in);
-        return;
+        return false;
     }
-    const float ix = 1.0f / dir.x, iy = 1.0f / dir.y, iz = 1.0f / dir.z;
-    const uint32_t oct = (ix < 0.0f ? 1u : 0u) | (iy < 0.0f ? 2u : 0u) | (iz < 0.0f ? 4u : 0u);
     // distance from o to any phantom point: |o - c| + radius + 2|o|
     const float dist = ((fabsf(org.x - p.tbvh_c[0]) + fabsf(org.y - p.tbvh_c[1])) +
                         fabsf(org.z - p.tbvh_c[2])) + p.tbvh_r + 2.0f * onorm;
-    const float rho = cam ? 0.0f : 1e-5f * ((dist + onorm) + p.tbvh_mag);
+    rho = cam ? 0.0f : 1e-5f * ((dist + onorm) + p.tbvh_mag);
+    return true;
+}
+
+// One node of the triangle tree (static or camera-origin).
+__device__ __forceinline__ void tri_step(const TraceParams &p, F3 org, F3 dir, F3 inv, uint32_t oct,
+                                         bool cam, float rho, float best_t, uint32_t &node,
+                                         float &tri_t, int &tri_i, uint32_t &tri_in,
+                                         uint32_t &node_tests, uint32_t &tri_done) {
+    ++node_tests;
     const float4 *nodes = cam ? p.cam_nodes : p.tbvh_nodes;
     const uint32_t *links = cam ? p.cam_miss : p.tbvh_miss;
-    const float4 *recs = cam ? p.cam_tris : p.tbvh_tris;
-    const uint32_t stride = cam ? 2u : 4u;
-    float cap = fminf(best_t, tri_t);
-    uint32_t node = 0;
-    while (node != kNodeEndDev) {
-        ++node_tests;
-        const float4 *nd = nodes + stride * node;
-        const float4 B0 = nd[0], B1 = nd[1];
-        float4 N0 = make_float4(0.0f, 0.0f, 0.0f, 0.0f), N1 = N0;  // camera tree: no widening
-        if (!cam) { N0 = nd[2]; N1 = nd[3]; }
-        const uint32_t miss = links[8u * node + oct];
-        // s = n^.o over the normal box
-        const float ax = N0.x * org.x, bx = N1.x * org.x;
-        const float ay = N0.y * org.y, by = N1.y * org.y;
-        const float az = N0.z * org.z, bz = N1.z * org.z;
-        const float sl = (fminf(ax, bx) + fminf(ay, by)) + fminf(az, bz);
-        const float sh = (fmaxf(ax, bx) + fmaxf(ay, by)) + fmaxf(az, bz);
-        // phantom offset 2 s m_k over s in [sl, sh], m_k in [N0.k, N1.k]
-        auto widen = [&](float lo, float hi, float m0, float m1, float o, float inv, float &t0,
-                         float &t1) {
-            const float a = sl * m0, b = sl * m1, c = sh * m0, d = sh * m1;
-            const float omin = fminf(fminf(a, b), fminf(c, d));
-            const float omax = fmaxf(fmaxf(a, b), fmaxf(c, d));
-            const float l = (lo + 2.0f * omin) - rho;
-            const float h = (hi + 2.0f * omax) + rho;
-            t0 = (l - o) * inv;
-            t1 = (h - o) * inv;
-        };
-        float t0x, t1x, t0y, t1y, t0z, t1z;
-        widen(B0.x, B1.x, N0.x, N1.x, org.x, ix, t0x, t1x);
-        widen(B0.y, B1.y, N0.y, N1.y, org.y, iy, t0y, t1y);
-        widen(B0.z, B1.z, N0.z, N1.z, org.z, iz, t0z, t1z);
-        const float tn = fmaxf(fmaxf(fminf(t0x, t1x), fminf(t0y, t1y)), fminf(t0z, t1z));
-        const float tf = fminf(fminf(fmaxf(t0x, t1x), fmaxf(t0y, t1y)), fmaxf(t0z, t1z));
-        const bool skip = tn > tf || tf < 0.001f || tn > cap;
-        const uint32_t a = __float_as_uint(B0.w);
-        const bool leaf = (a & kLeafBitDev) != 0;
-        const uint32_t child = a + ((oct >> __float_as_uint(B1.w)) & 1u);
-        const uint32_t next = (skip || leaf) ? miss : child;
-        if (!skip && leaf) {
-            const uint32_t first = a & ~kLeafBitDev, count = __float_as_uint(B1.w);
-            tri_done += count;
-            for (uint32_t j = first; j < first + count; ++j)
-                tri_record(recs + 4u * j, org, dir, best_t, tri_t, tri_i, tri_in);
-            cap = fminf(best_t, tri_t);
-        }
-        node = next;
+    const float4 *nd = nodes + (cam ? 2u : 4u) * node;
+    const float4 B0 = nd[0], B1 = nd[1];
+    float4 N0 = make_float4(0.0f, 0.0f, 0.0f, 0.0f), N1 = N0;  // camera tree: no widening
+    if (!cam) { N0 = nd[2]; N1 = nd[3]; }
+    const uint32_t miss = links[8u * node + oct];
+    // s = n^.o over the normal box
+    const float ax = N0.x * org.x, bx = N1.x * org.x;
+    const float ay = N0.y * org.y, by = N1.y * org.y;
+    const float az = N0.z * org.z, bz = N1.z * org.z;
+    const float sl = (fminf(ax, bx) + fminf(ay, by)) + fminf(az, bz);
+    const float sh = (fmaxf(ax, bx) + fmaxf(ay, by)) + fmaxf(az, bz);
+    // phantom offset 2 s m_k over s in [sl, sh], m_k in [N0.k, N1.k]
+    auto widen = [&](float lo, float hi, float m0, float m1, float o, float iv, float &t0, float &t1) {
+        const float a = sl * m0, b = sl * m1, c = sh * m0, d = sh * m1;
+        const float omin = fminf(fminf(a, b), fminf(c, d));
+        const float omax = fmaxf(fmaxf(a, b), fmaxf(c, d));
+        const float l = (lo + 2.0f * omin) - rho;
+        const float h = (hi + 2.0f * omax) + rho;
+        t0 = (l - o) * iv;
+        t1 = (h - o) * iv;
+    };
+    float t0x, t1x, t0y, t1y, t0z, t1z;
+    widen(B0.x, B1.x, N0.x, N1.x, org.x, inv.x, t0x, t1x);
+    widen(B0.y, B1.y, N0.y, N1.y, org.y, inv.y, t0y, t1y);
+    widen(B0.z, B1.z, N0.z, N1.z, org.z, inv.z, t0z, t1z);
+    const float tn = fmaxf(fmaxf(fminf(t0x, t1x), fminf(t0y, t1y)), fminf(t0z, t1z));
+    const float tf = fminf(fminf(fmaxf(t0x, t1x), fmaxf(t0y, t1y)), fmaxf(t0z, t1z));
+    const bool skip = tn > tf || tf < 0.001f || tn > fminf(best_t, tri_t);
+    const uint32_t a = __float_as_uint(B0.w);
+    const bool leaf = (a & kLeafBitDev) != 0;
+    const uint32_t child = a + ((oct >> __float_as_uint(B1.w)) & 1u);
+    node = (skip || leaf) ? miss : child;
+    if (!skip && leaf) {
+        const float4 *recs = cam ? p.cam_tris : p.tbvh_tris;
+        const uint32_t first = a & ~kLeafBitDev, count = __float_as_uint(B1.w);
+        tri_done += count;
+        for (uint32_t j = first; j < first + count; ++j)
+            tri_record(recs + 4u * j, org, dir, best_t, tri_t, tri_i, tri_in);
     }
 }
 
 // ------------------------------------------------------------ trace kernel
 // kBvh: sphere search through the exact BVH (else brute force).  kLds: the
 // tree is copied into the workgroup's LDS once (persistent grid), so every
-// traversal step is a ds_read instead of an L2 round trip.
-template <bool kBvh, bool kLds>
+// traversal step is a ds_read instead of an L2 round trip.  kStep: the BVH
+// walks are cut into slices of p.steps nodes, so lanes that finish early are
+// shaded and refilled while the wave's long walks continue (triangle scenes:
+// walk lengths vary by 10-100x); without it a lane walks to the end in one
+// iteration (cheaper per node: sphere-only scenes).
+template <bool kBvh, bool kLds, bool kStep>
 __global__ __launch_bounds__(kLds ? 512 : 256) void trace_kernel(TraceParams p) {
     const uint32_t lane = __lane_id();
     extern __shared__ float4 lds[];
@@ -437,9 +446,14 @@ __global__ __launch_bounds__(kLds ? 512 : 256) void trace_kernel(TraceParams p) 
                        p.sph_shade, p.sph_kind};
     }
 
-    F3 org = f3(0, 0, 0), dir = f3(0, 0, 0);
+    F3 org = f3(0, 0, 0), dir = f3(0, 0, 0), inv = f3(0, 0, 0);
     float thr_r = 1.0f, thr_g = 1.0f, thr_b = 1.0f;  // ray_color's final_color
     uint32_t rng = 0, slot = 0, bounce = 0;
+    // lane state between loop iterations (see the bounce loop below)
+    enum : uint32_t { kSetup = 0, kSph = 1, kTriInit = 2, kTri = 3, kShade = 4 };
+    uint32_t phase = kSetup, node = 0, oct = 0;
+    float best_t = 0.0f, tri_t = 0.0f, e = 0.0f;  // e: the triangle walk's margin rho
+    int best_i = -1, tri_i = -1;
     bool active = false;
     uint32_t rays = 0, tri_in = 0, sph_tests = 0, node_tests = 0, tnode_tests = 0,
              tri_done = 0;
@@ -514,6 +528,7 @@ __global__ __launch_bounds__(kLds ? 512 : 256) void trace_kernel(TraceParams p) 
                 dir = unit(((llc + scale(h, u)) + scale(vv, v)) - org);
                 thr_r = thr_g = thr_b = 1.0f;
                 bounce = 0;
+                phase = kSetup;
                 active = true;
             }
             pool_next += min(ndead, avail);
@@ -531,32 +546,74 @@ __global__ __launch_bounds__(kLds ? 512 : 256) void trace_kernel(TraceParams p) 
         }
         if (!active) continue;
 
-        // ---- one iteration of ray_color's bounce loop (common.rs:267-282) --
+        // ---- ray_color's bounce loop (common.rs:267-282) as a lane state
+        // machine: setup -> sphere walk -> triangle walk -> shade.  The walks
+        // advance at most p.steps nodes per loop iteration, so lanes whose
+        // search ends early are shaded and refilled while the others walk on.
         bool done = false;
         float out_r = 0.0f, out_g = 0.0f, out_b = 0.0f;
-        if ((int32_t)bounce >= p.depth) {
-            done = true;  // depth exhausted -> (0, 0, 0) (common.rs:284)
-        } else {
-            ++rays;
-            // World::hit, spheres in order with shrinking t_max (common.rs:241-247)
-            float best_t = __builtin_inff();
-            int best_i = -1;
-            if (kBvh) {
-                spheres_bvh<kLds>(p, view, org, dir, best_t, best_i, sph_tests, node_tests);
+        if (phase == kSetup) {
+            if ((int32_t)bounce >= p.depth) {
+                done = true;  // depth exhausted -> (0, 0, 0) (common.rs:284)
             } else {
-                spheres_brute(p, org, dir, best_t, best_i);
+                ++rays;
+                inv = f3(1.0f / dir.x, 1.0f / dir.y, 1.0f / dir.z);
+                oct = (inv.x < 0.0f ? 1u : 0u) | (inv.y < 0.0f ? 2u : 0u) | (inv.z < 0.0f ? 4u : 0u);
+                // World::hit, spheres in order with shrinking t_max (common.rs:241-247)
+                best_t = __builtin_inff();
+                best_i = -1;
+                if (kBvh) {
+                    spheres_big(p, org, dir, best_t, best_i);
+                    node = 0;
+                    // (RT_AMD_ABLATE=1: timing-only diagnostic, results are wrong)
+                    phase = (p.ablate & 1u) ? kTriInit : kSph;
+                } else {
+                    spheres_brute(p, org, dir, best_t, best_i);
+                    phase = kTriInit;
+                }
             }
-            RT_STAMP(1);
+        }
+        RT_STAMP(1);
+        // kStep: at most p.steps node visits per lane per iteration
+        uint32_t budget = p.steps;
+        if (kBvh && phase == kSph) {
+            constexpr uint32_t kEnd = kLds ? 0xFFFFu : kNodeEndDev;
+            const SphBound bnd = sph_bound(p, org);
+            const float e = sph_inflation(p, bnd, best_t);
+            F3 lo = f3(org.x + e, org.y + e, org.z + e), hi = f3(org.x - e, org.y - e, org.z - e);
+            do {
+                sphere_step<kLds>(p, view, org, dir, inv, oct, node, best_t, best_i, bnd, lo, hi,
+                                  sph_tests, node_tests);
+            } while (node != kEnd && (!kStep || --budget != 0));
+            if (node == kEnd) phase = kTriInit;
+        }
+        if (phase == kTriInit) {
             // Mesh::hit with t_max = best_t, own closest from +inf (common.rs:178-223)
-            float tri_t = __builtin_inff();
-            int tri_i = -1;
+            tri_t = __builtin_inff();
+            tri_i = -1;
+            phase = kShade;
             if (p.tnodes != 0) {
-                triangles_bvh(p, org, dir, best_t, bounce == 0 && p.cam_nnodes != 0, tri_t, tri_i,
-                              tri_in, tnode_tests, tri_done);
+                if (tri_begin(p, org, dir, best_t, bounce == 0 && p.cam_nnodes != 0, e, tri_t, tri_i,
+                              tri_in, tri_done)) {
+                    node = 0;
+                    phase = kTri;
+                }
             } else {
                 triangles_brute(p, org, dir, best_t, tri_t, tri_i, tri_in);
             }
-
+        }
+        if (phase == kTri) {
+            if (kStep) budget = max(budget, p.steps / 2u);  // a lane that just left the sphere walk
+            const bool cam = bounce == 0 && p.cam_nnodes != 0;
+            do {
+                tri_step(p, org, dir, inv, oct, cam, e, best_t, node, tri_t, tri_i, tri_in,
+                         tnode_tests, tri_done);
+            } while (node != kNodeEndDev && (!kStep || --budget != 0));
+            if (node == kNodeEndDev) phase = kShade;
+        }
+        RT_STAMP(2);
+        if (phase == kShade) {
+            phase = kSetup;
             if (tri_i < 0 && best_i < 0) {
                 // background (common.rs:276-281): re-normalise, lerp to sky blue
                 const float t = 0.5f * (unit(dir).y + 1.0f);
@@ -596,8 +653,8 @@ __global__ __launch_bounds__(kLds ? 512 : 256) void trace_kernel(TraceParams p) 
                     const F3 ru = draw_unit(rng);
                     if (kind == kMatDiffuse) {  // materials.rs:42-52
                         v = nrm + ru;
-                        const float e = 1e-8f;
-                        keep_normal = fabsf(v.x) < e && fabsf(v.y) < e && fabsf(v.z) < e;
+                        const float eps = 1e-8f;
+                        keep_normal = fabsf(v.x) < eps && fabsf(v.y) < eps && fabsf(v.z) < eps;
                     } else {  // materials.rs:54-63 (reflect, maths.rs:26-28)
                         const F3 refl = dir - scale(nrm, 2.0f * dot(dir, nrm));
                         v = refl + scale(ru, param);
@@ -630,12 +687,11 @@ __global__ __launch_bounds__(kLds ? 512 : 256) void trace_kernel(TraceParams p) 
                 }
             }
         }
-        RT_STAMP(2);
+        RT_STAMP(3);
         if (done) {
             p.samples[slot] = make_float4(out_r, out_g, out_b, 0.0f);
             active = false;
         }
-        RT_STAMP(3);
     }
 
     // ---- per-wave statistics: one atomic per counter per wave ------------
@@ -687,14 +743,20 @@ size_t trace_lds_bytes(const TraceParams &p) {
     return (size_t)p.nnodes * 48 + (size_t)p.nprims * 20 + (size_t)p.nsph_padded * 36;
 }
 
-hipError_t launch_trace(const TraceParams &p, uint32_t blocks, hipStream_t stream) {
+template <bool kStep>
+static void launch_trace_t(const TraceParams &p, uint32_t blocks, hipStream_t stream) {
     if (p.nnodes && p.use_lds)
-        hipLaunchKernelGGL((trace_kernel<true, true>), dim3(blocks), dim3(512), trace_lds_bytes(p),
-                           stream, p);
+        hipLaunchKernelGGL((trace_kernel<true, true, kStep>), dim3(blocks), dim3(512),
+                           trace_lds_bytes(p), stream, p);
     else if (p.nnodes)
-        hipLaunchKernelGGL((trace_kernel<true, false>), dim3(blocks), dim3(256), 0, stream, p);
+        hipLaunchKernelGGL((trace_kernel<true, false, kStep>), dim3(blocks), dim3(256), 0, stream, p);
     else
-        hipLaunchKernelGGL((trace_kernel<false, false>), dim3(blocks), dim3(256), 0, stream, p);
+        hipLaunchKernelGGL((trace_kernel<false, false, kStep>), dim3(blocks), dim3(256), 0, stream, p);
+}
+
+hipError_t launch_trace(const TraceParams &p, uint32_t blocks, hipStream_t stream) {
+    if (p.step) launch_trace_t<true>(p, blocks, stream);
+    else launch_trace_t<false>(p, blocks, stream);
     return hipGetLastError();
 }
 
@@ -707,14 +769,21 @@ hipError_t launch_resolve_ex(const float4 *samples, uint32_t *out, uint32_t npix
     return hipGetLastError();
 }
 
-hipError_t trace_occupancy(int *blocks_per_cu, int variant, size_t lds_bytes) {
+template <bool kStep>
+static hipError_t trace_occupancy_t(int *blocks_per_cu, int variant, size_t lds_bytes) {
     if (variant == 2)
-        return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, trace_kernel<true, true>,
-                                                            512, lds_bytes);
+        return hipOccupancyMaxActiveBlocksPerMultiprocessor(
+            blocks_per_cu, trace_kernel<true, true, kStep>, 512, lds_bytes);
     if (variant == 1)
-        return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, trace_kernel<true, false>,
-                                                            256, 0);
-    return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, trace_kernel<false, false>, 256, 0);
+        return hipOccupancyMaxActiveBlocksPerMultiprocessor(
+            blocks_per_cu, trace_kernel<true, false, kStep>, 256, 0);
+    return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu,
+                                                        trace_kernel<false, false, kStep>, 256, 0);
+}
+
+hipError_t trace_occupancy(int *blocks_per_cu, int variant, size_t lds_bytes, bool step) {
+    return step ? trace_occupancy_t<true>(blocks_per_cu, variant, lds_bytes)
+                : trace_occupancy_t<false>(blocks_per_cu, variant, lds_bytes);
 }
 
 }  // namespace rtamd

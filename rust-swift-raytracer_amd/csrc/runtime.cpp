@@ -91,8 +91,10 @@ static int device_for(WorldState &w, int want, DeviceState *&out) {
         hipDeviceProp_t prop;
         HIP_TRY(hipGetDeviceProperties(&prop, dev));
         d->num_cus = prop.multiProcessorCount;
-        HIP_TRY(trace_occupancy(&d->blocks_per_cu, 0, 0));
-        HIP_TRY(trace_occupancy(&d->blocks_per_cu_bvh, 1, 0));
+        for (int st = 0; st < 2; ++st) {
+            HIP_TRY(trace_occupancy(&d->blocks_per_cu[st], 0, 0, st));
+            HIP_TRY(trace_occupancy(&d->blocks_per_cu_bvh[st], 1, 0, st));
+        }
         // scene upload (once per device)
         const PackedScene &p = w.packed;
         auto up = [&](void **dst, const std::vector<float> &src) -> hipError_t {
@@ -140,8 +142,9 @@ static int device_for(WorldState &w, int want, DeviceState *&out) {
                     m16[i] = bv.miss[i] == kNodeEnd ? (uint16_t)0xFFFF : (uint16_t)bv.miss[i];
                 HIP_TRY(hipMalloc((void **)&d->bvh_miss16, m16.size() * 2));
                 HIP_TRY(hipMemcpy(d->bvh_miss16, m16.data(), m16.size() * 2, hipMemcpyHostToDevice));
-                HIP_TRY(trace_occupancy(&d->blocks_per_cu_lds, 2, lds));
-                if (d->blocks_per_cu_lds > 0) d->lds_bytes = lds;
+                for (int st = 0; st < 2; ++st)
+                    HIP_TRY(trace_occupancy(&d->blocks_per_cu_lds[st], 2, lds, st));
+                if (d->blocks_per_cu_lds[0] > 0 && d->blocks_per_cu_lds[1] > 0) d->lds_bytes = lds;
             }
         }
         const TriangleBVH &tb = w.tbvh;
@@ -160,9 +163,11 @@ static int device_for(WorldState &w, int want, DeviceState *&out) {
             d->tloose = (uint32_t)tb.loose.size();
         }
         const uint64_t bpc = env_u64("RT_AMD_BLOCKS_PER_CU", 0);
-        if (bpc) d->blocks_per_cu = d->blocks_per_cu_bvh = d->blocks_per_cu_lds = (int)bpc;
-        if (d->blocks_per_cu < 1) d->blocks_per_cu = 1;
-        if (d->blocks_per_cu_bvh < 1) d->blocks_per_cu_bvh = 1;
+        for (int st = 0; st < 2; ++st) {
+            if (bpc) d->blocks_per_cu[st] = d->blocks_per_cu_bvh[st] = d->blocks_per_cu_lds[st] = (int)bpc;
+            d->blocks_per_cu[st] = std::max(d->blocks_per_cu[st], 1);
+            d->blocks_per_cu_bvh[st] = std::max(d->blocks_per_cu_bvh[st], 1);
+        }
         HIP_TRY(hipMalloc((void **)&d->counter, 64));
         HIP_TRY(hipMalloc((void **)&d->stats, 128));
         slot = std::move(d);
@@ -252,6 +257,7 @@ int render_frame(WorldState &w, const CameraModel &cam, size_t width, size_t hei
     p.div_width = make_fastdiv((uint32_t)width);
     p.div_rowblock = make_fastdiv(B);
     p.refill_min = (uint32_t)std::max<uint64_t>(1, env_u64("RT_AMD_REFILL", 1));
+    p.steps = (uint32_t)std::max<uint64_t>(1, env_u64("RT_AMD_STEPS", 256));
     p.row_block = B; p.rank = o.rank; p.nranks = nranks;
     const bool use_bvh = d->nnodes > 0 && o.accel != RT_ACCEL_BRUTE;
     if (use_bvh) {
@@ -299,7 +305,10 @@ int render_frame(WorldState &w, const CameraModel &cam, size_t width, size_t hei
     }
     const float inv_spp = 1.0f / (float)o.samples_per_pixel;  // 1.0 / spp as f32 (common.rs:345)
 
-    const int bpc = !use_bvh ? d->blocks_per_cu : p.use_lds ? d->blocks_per_cu_lds : d->blocks_per_cu_bvh;
+    // sliced walks pay off when walk lengths vary a lot: scenes with a triangle tree
+    p.step = (uint32_t)env_u64("RT_AMD_STEP", use_tbvh ? 1 : 0) != 0;
+    const int sv = p.step ? 1 : 0;
+    const int bpc = !use_bvh ? d->blocks_per_cu[sv] : p.use_lds ? d->blocks_per_cu_lds[sv] : d->blocks_per_cu_bvh[sv];
     const uint64_t waves_per_block = (use_bvh && p.use_lds) ? 8 : 4;
     const uint64_t full_blocks = (uint64_t)bpc * (uint64_t)d->num_cus;
     double trace_ms = 0.0, resolve_ms = 0.0;

@@ -48,7 +48,9 @@ struct DeviceState {
     uint32_t *replay = nullptr;      size_t replay_cap = 0;
     uint32_t *counter = nullptr;                                // job counter
     unsigned long long *stats = nullptr;                        // TraceParams::stats (16 slots)
-    int blocks_per_cu = 0, blocks_per_cu_bvh = 0, blocks_per_cu_lds = 0, num_cus = 0;
+    // resident workgroups per CU of each kernel variant, [0]: whole walks, [1]: sliced walks
+    int blocks_per_cu[2] = {0, 0}, blocks_per_cu_bvh[2] = {0, 0}, blocks_per_cu_lds[2] = {0, 0};
+    int num_cus = 0;
     size_t last_jobs = 0;                                       // jobs of the last launch
     ~DeviceState();
 };

@@ -21,4 +21,6 @@ run pmc_fetch 600 --kernel-trace --pmc FETCH_SIZE
 run pmc_write 600 --kernel-trace --pmc WRITE_SIZE
 run pmc_valu 600 --kernel-trace --pmc SQ_INSTS_VALU SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_VALU SQ_INSTS_SALU
 run pmc_wait 600 --kernel-trace --pmc SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE
+run pmc_l2 600 --kernel-trace --pmc TCC_HIT_sum TCC_MISS_sum TCC_REQ_sum
+run pmc_tcp 600 --kernel-trace --pmc TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_READ_REQ_sum SQ_INSTS_VMEM_RD TCP_PENDING_STALL_CYCLES_sum
 find "$OUT" -name "*.csv" | head -20
