@@ -277,14 +277,27 @@ static std::vector<float> triangle_records(const std::vector<Prim> &prims,
 }
 
 TriangleBVH build_triangle_bvh(const std::vector<Triangle> &tris, const std::vector<float> &tri_hot,
-                               uint32_t leaf_size) {
+                               uint32_t leaf_size, const float *oc, double phantom) {
     TriangleBVH out;
+    if (oc)
+        for (int k = 0; k < 3; ++k) out.oc[k] = oc[k];
     std::vector<Prim> prims;
+    std::vector<Prim> geo_prims;  // unshifted, for the centre / radius bound
     for (uint32_t i = 0; i < tris.size(); ++i) {
         Prim p;
         const int kind = triangle_prim(tris[i], &tri_hot[(size_t)i * 4], i, p);
-        if (kind == 0) prims.push_back(p);
-        else if (kind == 2) out.loose.push_back(i);
+        if (kind == 2) out.loose.push_back(i);
+        if (kind != 0) continue;
+        geo_prims.push_back(p);
+        if (oc) {  // phantoms of origin oc: + 2(n^.oc)n^ (exact in double, rounded outward below)
+            const double sdot = p.n[0] * oc[0] + p.n[1] * oc[1] + p.n[2] * oc[2];
+            for (int k = 0; k < 3; ++k) {
+                p.box.lo[k] += 2 * sdot * p.n[k];
+                p.box.hi[k] += 2 * sdot * p.n[k];
+                p.c[k] = (p.box.lo[k] + p.box.hi[k]) / 2;
+            }
+        }
+        prims.push_back(p);
     }
     if (prims.size() < 16) {  // not worth a tree: brute force keeps the reference order
         out.loose.clear();
@@ -301,6 +314,7 @@ TriangleBVH build_triangle_bvh(const std::vector<Triangle> &tris, const std::vec
     }
     double L = 0.4 * (std::sqrt(cn) + hd / 2);  // A/B on C5 (tools/tbvh_sim.cpp): 1-4 best
     if (const char *e = std::getenv("RT_AMD_TRI_PHANTOM")) L = std::atof(e);
+    if (phantom > 0) L = phantom;
     Builder b(prims, std::max(1u, leaf_size), L > 0 ? L : 1e-30);
     b.nodes.reserve(prims.size() * 2);
     b.nodes.emplace_back();
@@ -311,10 +325,11 @@ TriangleBVH build_triangle_bvh(const std::vector<Triangle> &tris, const std::vec
 
     Box all;
     double mag = 0;
-    for (const Prim &p : prims) {
+    for (const Prim &p : geo_prims) {
         all.grow(p.box);
         for (int k = 0; k < 3; ++k) mag = std::max({mag, std::fabs(p.box.lo[k]), std::fabs(p.box.hi[k])});
     }
+    for (int k = 0; k < 3; ++k) mag = std::max(mag, (double)std::fabs(out.oc[k]));
     double half = 0;
     for (int k = 0; k < 3; ++k) {
         out.centre[k] = (float)((all.lo[k] + all.hi[k]) / 2);

@@ -57,12 +57,18 @@ struct TriangleBVH {
     std::vector<uint32_t> loose;    // brute-forced triangles (non-finite data, slivers)
     float centre[3] = {0, 0, 0};
     float radius = 0, mag = 0;      // vertices within radius of centre; max |coordinate|
+    // Boxes hold the phantoms for origin oc; the kernel widens them by
+    // 2(n^.d)n^ with d = o - oc (oc = 0: the plain tree).
+    float oc[3] = {0, 0, 0};
     uint32_t depth = 0;
 };
 
 // tri_hot: PackedScene::tri_hot (the exact per-triangle n and n.v0 bits).
+// oc (optional): origin the boxes are built for; phantom: SAH weight of the
+// normal spread (<= 0: derived from the scene).
 TriangleBVH build_triangle_bvh(const std::vector<Triangle> &tris, const std::vector<float> &tri_hot,
-                               uint32_t leaf_size);
+                               uint32_t leaf_size, const float *oc = nullptr,
+                               double phantom = 0);
 
 // Primary rays all start at the camera origin, so their phantom triangles are
 // fixed: this tree holds, per triangle of `tb`, its box translated by

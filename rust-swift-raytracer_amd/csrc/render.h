@@ -60,6 +60,7 @@ struct TraceParams {
     const uint32_t *tbvh_loose;  // triangles tested by brute force, ascending
     uint32_t tnodes, ttris, tloose;
     float tbvh_c[3], tbvh_r, tbvh_mag;
+    float tbvh_oc[3];         // origin the boxes were built for (widening uses o - oc)
     // the same triangles' phantoms for the camera origin (bvh.h CameraTriangleBVH),
     // used at bounce 0; cam_nnodes == 0: bounce 0 uses the tree above
     const float4 *cam_nodes;  // 2 per node

@@ -357,8 +357,8 @@ __device__ __forceinline__ bool tri_begin(const TraceParams &p, F3 org, F3 dir, 
 }
 
 // One node of the triangle tree (static or camera-origin).
-__device__ __forceinline__ void tri_step(const TraceParams &p, F3 org, F3 dir, F3 inv, uint32_t oct,
-                                         bool cam, float rho, float best_t, uint32_t &node,
+__device__ __forceinline__ void tri_step(const TraceParams &p, F3 org, F3 dir, F3 inv, F3 dlt,
+                                         uint32_t oct, bool cam, float rho, float best_t, uint32_t &node,
                                          float &tri_t, int &tri_i, uint32_t &tri_in,
                                          uint32_t &node_tests, uint32_t &tri_done) {
     ++node_tests;
@@ -369,10 +369,10 @@ __device__ __forceinline__ void tri_step(const TraceParams &p, F3 org, F3 dir, F
     float4 N0 = make_float4(0.0f, 0.0f, 0.0f, 0.0f), N1 = N0;  // camera tree: no widening
     if (!cam) { N0 = nd[2]; N1 = nd[3]; }
     const uint32_t miss = links[8u * node + oct];
-    // s = n^.o over the normal box
-    const float ax = N0.x * org.x, bx = N1.x * org.x;
-    const float ay = N0.y * org.y, by = N1.y * org.y;
-    const float az = N0.z * org.z, bz = N1.z * org.z;
+    // s = n^.d over the normal box, d = o - oc (the tree's box origin, bvh.h)
+    const float ax = N0.x * dlt.x, bx = N1.x * dlt.x;
+    const float ay = N0.y * dlt.y, by = N1.y * dlt.y;
+    const float az = N0.z * dlt.z, bz = N1.z * dlt.z;
     const float sl = (fminf(ax, bx) + fminf(ay, by)) + fminf(az, bz);
     const float sh = (fmaxf(ax, bx) + fmaxf(ay, by)) + fmaxf(az, bz);
     // phantom offset 2 s m_k over s in [sl, sh], m_k in [N0.k, N1.k]
@@ -605,8 +605,9 @@ __global__ __launch_bounds__(kLds ? 512 : 256) void trace_kernel(TraceParams p) 
         if (phase == kTri) {
             if (kStep) budget = max(budget, p.steps / 2u);  // a lane that just left the sphere walk
             const bool cam = bounce == 0 && p.cam_nnodes != 0;
+            const F3 dlt = f3(org.x - p.tbvh_oc[0], org.y - p.tbvh_oc[1], org.z - p.tbvh_oc[2]);
             do {
-                tri_step(p, org, dir, inv, oct, cam, e, best_t, node, tri_t, tri_i, tri_in,
+                tri_step(p, org, dir, inv, dlt, oct, cam, e, best_t, node, tri_t, tri_i, tri_in,
                          tnode_tests, tri_done);
             } while (node != kNodeEndDev && (!kStep || --budget != 0));
             if (node == kNodeEndDev) phase = kShade;

@@ -300,7 +300,7 @@ int render_frame(WorldState &w, const CameraModel &cam, size_t width, size_t hei
         p.tbvh_nodes = d->tbvh_nodes; p.tbvh_miss = d->tbvh_miss;
         p.tbvh_tris = d->tbvh_tris; p.tbvh_loose = d->tbvh_loose;
         p.tnodes = d->tnodes; p.ttris = d->ttris; p.tloose = d->tloose;
-        for (int k = 0; k < 3; ++k) p.tbvh_c[k] = tb.centre[k];
+        for (int k = 0; k < 3; ++k) { p.tbvh_c[k] = tb.centre[k]; p.tbvh_oc[k] = tb.oc[k]; }
         p.tbvh_r = tb.radius; p.tbvh_mag = tb.mag;
     }
     const float inv_spp = 1.0f / (float)o.samples_per_pixel;  // 1.0 / spp as f32 (common.rs:345)

@@ -9,6 +9,9 @@
 #include <cstdio>
 #include <cstdlib>
 #include <fstream>
+#include <map>
+#include <tuple>
+#include <vector>
 #include <sstream>
 
 #include "bvh.h"
@@ -42,8 +45,9 @@ static float trace(const TriangleBVH &t, V o, V d, Count &c) {
         const float *n = &t.nodes[(size_t)node * 16];
         float sl = 0, sh = 0;
         const float ov[3] = {o.x, o.y, o.z}, iv[3] = {ix, iy, iz};
+        const float dv[3] = {o.x - t.oc[0], o.y - t.oc[1], o.z - t.oc[2]};
         for (int k = 0; k < 3; ++k) {
-            float a = n[8 + k] * ov[k], b = n[12 + k] * ov[k];
+            float a = n[8 + k] * dv[k], b = n[12 + k] * dv[k];
             sl += std::fmin(a, b); sh += std::fmax(a, b);
         }
         if (g_exact) sl = sh = 0;
@@ -134,6 +138,40 @@ int main(int argc, char **argv) {
                 trace(t, o2, d2, sec);
             }
         }
+    if (const char *cs = std::getenv("SIM_CELL")) {  // per-cell trees for the secondary rays
+        const float S = std::atof(cs);
+        // secondary origins: the primary hit points (recomputed)
+        std::vector<V> o2s, d2s;
+        uint32_t rng2 = 2547549u;
+        auto rnd2 = [&]() { rng2 ^= rng2 << 13; rng2 ^= rng2 >> 17; rng2 ^= rng2 << 5; return rng2 * 0x1p-32f; };
+        Count dummy;
+        for (int j = 0; j < H; ++j)
+            for (int i = 0; i < W; ++i) {
+                float u = (i + 0.5f) / W, v = (j + 0.5f) / H;
+                V d = unit(sub(add(add(V{cm.lower_left.x, cm.lower_left.y, cm.lower_left.z},
+                                       mul(V{cm.horizontal.x, cm.horizontal.y, cm.horizontal.z}, u)),
+                                   mul(V{cm.vertical.x, cm.vertical.y, cm.vertical.z}, v)), org));
+                float tt = trace(t, org, d, dummy);
+                if (std::isfinite(tt)) {
+                    o2s.push_back(add(org, mul(d, tt)));
+                    d2s.push_back(unit(V{rnd2() * 2 - 1, rnd2() * 2 - 1, rnd2() * 2 - 1}));
+                }
+            }
+        std::map<std::tuple<int, int, int>, TriangleBVH> trees;
+        Count cell;
+        for (size_t r = 0; r < o2s.size(); ++r) {
+            V o2 = o2s[r];
+            auto key = std::make_tuple((int)std::floor(o2.x / S), (int)std::floor(o2.y / S), (int)std::floor(o2.z / S));
+            auto it = trees.find(key);
+            if (it == trees.end()) {
+                float oc[3] = {(std::get<0>(key) + 0.5f) * S, (std::get<1>(key) + 0.5f) * S, (std::get<2>(key) + 0.5f) * S};
+                it = trees.emplace(key, build_triangle_bvh(s.triangles, p.tri_hot, lf ? std::atoi(lf) : 4, oc, S * 0.866)).first;
+            }
+            trace(it->second, o2, d2s[r], cell);
+        }
+        std::printf("cells S=%g: %zu trees, secondary %.1f nodes/ray, %.1f tests/ray\n", S, trees.size(),
+                    cell.nodes / cell.rays, cell.tests / cell.rays);
+    }
     std::printf("primary: %.0f rays, %.1f nodes/ray, %.1f tests/ray, hit %.3f\n", prim.rays,
                 prim.nodes / prim.rays, prim.tests / prim.rays, hits / prim.rays);
     if (sec.rays)
