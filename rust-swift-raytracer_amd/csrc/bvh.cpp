@@ -438,10 +438,11 @@ SphereBVH build_sphere_bvh(const std::vector<Sphere> &spheres, uint32_t leaf_siz
     out.depth = b.max_depth;
 
     Box all;
-    double rmax = 0, mag = 0;
+    double rmax = 0, rmin = std::numeric_limits<double>::infinity(), mag = 0;
     for (const Prim &p : prims) {
         all.grow(p.c);
         rmax = std::max(rmax, (p.box.hi[0] - p.box.lo[0]) / 2);
+        rmin = std::min(rmin, (p.box.hi[0] - p.box.lo[0]) / 2);
         for (int k = 0; k < 3; ++k) mag = std::max({mag, std::fabs(p.box.lo[k]), std::fabs(p.box.hi[k])});
     }
     double half = 0;
@@ -451,6 +452,8 @@ SphereBVH build_sphere_bvh(const std::vector<Sphere> &spheres, uint32_t leaf_siz
     }
     out.radius = up(half * std::sqrt(3.0) * (1 + 1e-6));
     out.rmax = up(rmax);
+    // 1/rmin rounded up (rmin rounded down); inf when some radius is 0
+    out.inv_rmin = rmin > 0 ? up(1.0 / (double)down(rmin)) : std::numeric_limits<float>::infinity();
     out.mag = up(mag);
 
     out.nodes.resize(b.nodes.size() * 8);

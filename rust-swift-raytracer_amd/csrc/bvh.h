@@ -32,9 +32,10 @@ struct SphereBVH {
     std::vector<uint32_t> prim_id;  // original sphere index (tie-break, shading)
     std::vector<uint32_t> big;      // spheres always tested by brute force (ascending)
     // Per-ray inflation inputs (all rounded up): |o - c| <= |o - centre| + radius
-    // for every BVH sphere; rmax = largest BVH radius; mag = largest |coordinate|.
+    // for every BVH sphere; rmax = largest BVH radius; mag = largest |coordinate|;
+    // inv_rmin >= 1 / smallest BVH radius (the quadratic bound).
     float centre[3] = {0, 0, 0};
-    float radius = 0, rmax = 0, mag = 0;
+    float radius = 0, rmax = 0, mag = 0, inv_rmin = 0;
     uint32_t depth = 0;
 };
 

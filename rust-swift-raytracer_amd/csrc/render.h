@@ -52,7 +52,7 @@ struct TraceParams {
     uint32_t refill_min;      // refill dead lanes once at least this many are idle
     uint32_t steps;           // BVH nodes a lane walks per loop iteration (>= 1) ...
     uint32_t step;            // ... when nonzero (else walks run to the end)
-    float bvh_c[3], bvh_r, bvh_rmax, bvh_mag;
+    float bvh_c[3], bvh_r, bvh_rmax, bvh_mag, bvh_inv_rmin;
     // phantom-aware triangle BVH (bvh.h TriangleBVH); tnodes == 0: brute-force Mesh loop
     const float4 *tbvh_nodes; // 4 per node: (min, a) (max, b) (normal min) (normal max)
     const uint32_t *tbvh_miss;// 8 per node

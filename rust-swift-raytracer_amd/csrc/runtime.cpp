@@ -270,6 +270,7 @@ int render_frame(WorldState &w, const CameraModel &cam, size_t width, size_t hei
         p.use_lds = d->lds_bytes > 0 && env_u64("RT_AMD_LDS", 1) != 0;
         for (int k = 0; k < 3; ++k) p.bvh_c[k] = bv.centre[k];
         p.bvh_r = bv.radius; p.bvh_rmax = bv.rmax; p.bvh_mag = bv.mag;
+        p.bvh_inv_rmin = env_u64("RT_AMD_LINEAR_E", 0) ? INFINITY : bv.inv_rmin;
     }
     const bool use_tbvh = d->tnodes > 0 && o.accel != RT_ACCEL_BRUTE;
     if (use_tbvh) prepare_camera(w, cam);
