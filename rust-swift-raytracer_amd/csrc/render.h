@@ -20,7 +20,7 @@ struct TraceParams {
     const float4 *tri_geo;    // ntri x 4: (v0, mat) (v1, 0) (v2, 0) (unit normal, 0)
     const float *mats;        // 8 floats per material: kind bits, r, g, b, param
     float4 *samples;          // slab-local per-sample colour (r, g, b, 0)
-    uint32_t *job_counter;    // zeroed before every launch
+    uint32_t *job_counter;    // nparts counters, 32 u32 apart; zeroed before every launch
     unsigned long long *stats;// rays, tri in t-range, BVH sphere tests, BVH node tests,
                               // 4 stamp counters, triangle-BVH node tests
     const uint32_t *replay;   // REPLAY start states (global job index)
@@ -35,6 +35,7 @@ struct TraceParams {
     uint32_t njobs;           // samples in this launch
     uint32_t npix;            // pixels in this launch (slab index = s*npix + pixel)
     uint32_t chunk;           // jobs fetched per atomic by one wave
+    uint32_t nparts;          // job-queue partitions (kernel header comment)
     // exact-pruning BVH (bvh.h); nnodes == 0 selects the brute-force kernel
     const float4 *bvh_nodes;  // 2 per node
     const uint32_t *bvh_miss; // 8 per node (one DFS successor per ray octant)

@@ -427,8 +427,14 @@ __device__ __forceinline__ void tri_leaf(const TraceParams &p, F3 org, F3 dir, b
 // shaded and refilled while the wave's long walks continue (triangle scenes:
 // walk lengths vary by 10-100x); without it a lane walks to the end in one
 // iteration (cheaper per node: sphere-only scenes).
+// 6 waves per SIMD = 80 VGPRs: 3 LDS workgroups of 512 per CU (A/B: 5 waves ->
+// 2 workgroups costs ~6% at C2)
+#ifndef RT_WAVES_PER_EU
+#define RT_WAVES_PER_EU 6
+#endif
 template <bool kBvh, bool kLds, bool kStep>
-__global__ __launch_bounds__(kLds ? 512 : 256) void trace_kernel(TraceParams p) {
+__global__ __launch_bounds__(kLds ? 512 : 256)
+__attribute__((amdgpu_waves_per_eu(RT_WAVES_PER_EU, 8))) void trace_kernel(TraceParams p) {
     const uint32_t lane = __lane_id();
     extern __shared__ float4 lds[];
     BvhView view;
@@ -492,7 +498,17 @@ __global__ __launch_bounds__(kLds ? 512 : 256) void trace_kernel(TraceParams p) 
     do {            \
     } while (0)
 #endif
-    uint32_t prefetch = 0;         // lane 0: base of the next chunk, fetched early
+    // Job queue: the launch's jobs are split into p.nparts equal partitions,
+    // each with its own counter on its own 128-B line (one shared counter
+    // serialises at ~12 ns per atomic: 6 ms per C2 frame).  A wave starts on
+    // its home partition and moves on when that one is drained.
+    uint32_t part = (blockIdx.x * (blockDim.x / kWave) + threadIdx.x / kWave) % p.nparts;
+    uint32_t tries = 0;  // partitions found drained (wave-uniform)
+    auto part_begin = [&](uint32_t k) -> uint32_t {
+        return (uint32_t)(((uint64_t)k * p.njobs) / p.nparts);
+    };
+    uint32_t pbegin = part_begin(part), pend = part_begin(part + 1);
+    uint32_t prefetch = 0;          // lane 0: counter value of the next chunk, fetched early
     bool prefetch_pending = false;  // wave-uniform
     for (;;) {
         // ---- refill lanes whose path ended (active-ray compaction) -------
@@ -500,15 +516,28 @@ __global__ __launch_bounds__(kLds ? 512 : 256) void trace_kernel(TraceParams p) 
         const uint32_t ndead = (uint32_t)__popcll(dead);
         if (dead != 0 && !exhausted && (ndead >= p.refill_min || ndead == kWave)) {
             if (pool_next >= pool_end) {
-                uint32_t base = prefetch;
-                if (!prefetch_pending && lane == 0) base = atomicAdd(p.job_counter, p.chunk);
+                uint32_t base = 0;
+                if (lane == 0) {
+                    base = pbegin + (prefetch_pending ? prefetch
+                                                      : atomicAdd(p.job_counter + 32u * part, p.chunk));
+                    while (base >= pend && ++tries < p.nparts) {
+                        part = part + 1 == p.nparts ? 0 : part + 1;
+                        pbegin = part_begin(part);
+                        pend = part_begin(part + 1);
+                        base = pbegin + atomicAdd(p.job_counter + 32u * part, p.chunk);
+                    }
+                }
                 prefetch_pending = false;
                 base = __builtin_amdgcn_readfirstlane(base);
-                if (base >= p.njobs) {
+                part = __builtin_amdgcn_readfirstlane(part);
+                tries = __builtin_amdgcn_readfirstlane(tries);
+                pbegin = __builtin_amdgcn_readfirstlane(pbegin);
+                pend = __builtin_amdgcn_readfirstlane(pend);
+                if (base >= pend) {
                     exhausted = true;
                 } else {
                     pool_next = base;
-                    pool_end = min(base + p.chunk, p.njobs);
+                    pool_end = min(base + p.chunk, pend);
                 }
             }
             const uint32_t avail = pool_end - pool_next;
@@ -549,7 +578,7 @@ __global__ __launch_bounds__(kLds ? 512 : 256) void trace_kernel(TraceParams p) 
             // ask for the next chunk now; the reply is only waited for when the
             // pool runs dry (hides the ~1-3 us atomic round trip)
             if (!exhausted && !prefetch_pending && pool_end - pool_next < kWave) {
-                if (lane == 0) prefetch = atomicAdd(p.job_counter, p.chunk);
+                if (lane == 0) prefetch = atomicAdd(p.job_counter + 32u * part, p.chunk);
                 prefetch_pending = true;
             }
         }

@@ -69,6 +69,8 @@ size_t tile_row(size_t k, uint32_t row_block, uint32_t rank, uint32_t nranks) {
     return ((k / B) * nranks + rank) * B + k % B;
 }
 
+static constexpr uint64_t kMaxParts = 1024;  // job-queue partitions (render.hip)
+
 static int device_for(WorldState &w, int want, DeviceState *&out) {
     int count = 0;
     if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) {
@@ -168,7 +170,7 @@ static int device_for(WorldState &w, int want, DeviceState *&out) {
             d->blocks_per_cu[st] = std::max(d->blocks_per_cu[st], 1);
             d->blocks_per_cu_bvh[st] = std::max(d->blocks_per_cu_bvh[st], 1);
         }
-        HIP_TRY(hipMalloc((void **)&d->counter, 64));
+        HIP_TRY(hipMalloc((void **)&d->counter, kMaxParts * 128));
         HIP_TRY(hipMalloc((void **)&d->stats, 128));
         slot = std::move(d);
     }
@@ -330,7 +332,11 @@ int render_frame(WorldState &w, const CameraModel &cam, size_t width, size_t hei
             uint64_t chunk = env_u64("RT_AMD_CHUNK", 0);
             if (!chunk) chunk = std::min<uint64_t>(256, std::max<uint64_t>(64, njobs / (nwaves * 16) / 64 * 64));
             p.chunk = (uint32_t)chunk;
-            HIP_TRY(hipMemsetAsync(d->counter, 0, 4, s));
+            // job-queue partitions: each keeps >= 16 chunks
+            uint64_t parts = env_u64("RT_AMD_PARTS", 64);
+            parts = std::max<uint64_t>(1, std::min<uint64_t>({parts, kMaxParts, njobs / (16 * chunk) + 1}));
+            p.nparts = (uint32_t)parts;
+            HIP_TRY(hipMemsetAsync(d->counter, 0, parts * 128, s));
             HIP_TRY(launch_trace(p, (uint32_t)blocks, s));
             d->last_jobs = njobs;
             ++launches;
