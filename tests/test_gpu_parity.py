@@ -209,6 +209,28 @@ def test_slabs_do_not_change_the_frame(monkeypatch):
     assert_bits_equal(many, one, "slabbed frame")
 
 
+@pytest.mark.parametrize("scene", ["rtow", "mesh_soup"])
+def test_scheduling_knobs_do_not_change_samples(monkeypatch, scene):
+    """Job-queue partitions, chunk size and walk slicing only reorder work:
+    every sample colour must be identical."""
+    src = scene_text("rtow.txt") if scene == "rtow" else _triangle_scene(41, 400, spheres=40)
+    w, h, spp = 160, 90, 4
+    world = R.World(src)
+    ref, _ = world.render(w, h, spp, 8)
+    ref_s = world.read_samples(w * h * spp)
+    for env in [dict(RT_AMD_PARTS="1"), dict(RT_AMD_PARTS="7", RT_AMD_CHUNK="64"),
+                dict(RT_AMD_PARTS="1024"), dict(RT_AMD_STEP="1", RT_AMD_STEPS="1"),
+                dict(RT_AMD_STEP="1", RT_AMD_STEPS="5"), dict(RT_AMD_STEP="0"),
+                dict(RT_AMD_REFILL="17")]:
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
+        out, _ = world.render(w, h, spp, 8)
+        assert_bits_equal(out, ref, f"frame {env}")
+        assert_bits_equal(world.read_samples(w * h * spp), ref_s, f"samples {env}")
+        for k in env:
+            monkeypatch.delenv(k)
+
+
 def test_full_size_c2_properties():
     """BASELINE configs[1] at full size: determinism + oracle parity on rows."""
     src = S.rtow()
