@@ -600,7 +600,11 @@ __attribute__((amdgpu_waves_per_eu(RT_WAVES_PER_EU, 8))) void trace_kernel(Trace
                 done = true;  // depth exhausted -> (0, 0, 0) (common.rs:284)
             } else {
                 ++rays;
-                inv = f3(1.0f / dir.x, 1.0f / dir.y, 1.0f / dir.z);
+                // slab-test reciprocals only (not reference arithmetic): v_rcp_f32's
+                // 1-ulp error moves a slab face by <= 4u|b - lo|, inside e_abs and
+                // rho; +-0 -> +-inf as with a divide
+                inv = f3(__builtin_amdgcn_rcpf(dir.x), __builtin_amdgcn_rcpf(dir.y),
+                         __builtin_amdgcn_rcpf(dir.z));
                 oct = (inv.x < 0.0f ? 1u : 0u) | (inv.y < 0.0f ? 2u : 0u) | (inv.z < 0.0f ? 4u : 0u);
                 // World::hit, spheres in order with shrinking t_max (common.rs:241-247)
                 best_t = __builtin_inff();
