@@ -46,7 +46,7 @@ SphereBVH build_sphere_bvh(const std::vector<Sphere> &spheres, uint32_t leaf_siz
 // triangle translated by 2(n^.o)n^ -- a "phantom" copy that depends on the
 // ray origin o.  Each node therefore also stores the box of its triangles'
 // unit normals; the kernel widens the node box per ray by the interval of
-// 2(n^.o)n^ over that normal box plus a rounding margin (DESIGN.md 5.2).
+// 2(n^.o)n^ over that normal box plus a rounding margin (DESIGN.md 5.3).
 // Nodes: four float4 -- (min.xyz, a) (max.xyz, b) (nmin.xyz, 0) (nmax.xyz, 0)
 // with a/b as in SphereBVH.
 struct TriangleBVH {

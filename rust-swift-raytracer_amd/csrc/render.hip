@@ -13,7 +13,8 @@
 // Work decomposition: one job = one pixel sample.  Each wave is
 // persistent: its 64 lanes trace one bounce per loop iteration; a lane whose
 // path ends writes the sample colour to a per-sample slab in HBM and takes
-// the next job (ballot + mbcnt prefix, one atomic per 256 jobs per wave), so
+// the next job (ballot + mbcnt prefix, one atomic per chunk per wave on one of
+// 64 partitioned counters), so
 // lanes never idle behind the longest path of their wave.  Spheres are read
 // with wave-uniform scalar loads (SGPR operands, scalar cache), never per lane.
 // The resolve kernel sums each pixel's samples in sample order (the
@@ -163,7 +164,7 @@ __device__ __forceinline__ bool sphere_candidate(float4 S, F3 org, F3 dir, int i
     return take;
 }
 
-constexpr float kErrK = 3.0e-3f;  // >= 2.7x the derived sqrt(30u) = 1.12e-3 (DESIGN.md 5.3)
+constexpr float kErrK = 3.0e-3f;  // >= 2.7x the derived sqrt(30u) = 1.12e-3 (DESIGN.md 5.2)
 
 // Where the traversal reads the tree from: global memory (any size) or the
 // workgroup's LDS copy (staged once per persistent workgroup).
@@ -324,7 +325,7 @@ __device__ __forceinline__ bool tri_record(const float4 *r, F3 org, F3 dir, floa
 // rounding.  Per node the kernel bounds s = n^.o over the node's normal box,
 // widens the box by the interval of 2 s m_k on each axis k (m over the normal
 // box) plus rho, a rounding margin that dominates every error term
-// (<= ~40u (dist + |o| + M), DESIGN.md 5.4), and skips only nodes the ray
+// (<= ~40u (dist + |o| + M), DESIGN.md 5.3), and skips only nodes the ray
 // certainly misses or enters beyond min(best_t, tri_t).
 //
 // cam (bounce 0, org == camera origin): the lane walks the camera-origin tree
