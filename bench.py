@@ -106,9 +106,17 @@ def main():
     world_size = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    # rehearsal knobs for a 1-GPU box (never set by the driver): all ranks on
+    # device 0 and gloo collectives, to exercise the N>1 path end to end
+    if os.environ.get("RT_BENCH_ONE_DEVICE") == "1":
+        local_rank = 0
+    backend = os.environ.get("RT_BENCH_BACKEND", "nccl")
     torch.cuda.set_device(local_rank)
     if world_size > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        else:
+            dist.init_process_group(backend)
 
     make_scene, W, H, spp, depth = S.CONFIGS[args.config]
     accel = {"auto": R.ACCEL_AUTO, "brute": R.ACCEL_BRUTE, "bvh": R.ACCEL_BVH}[args.accel]
@@ -127,7 +135,10 @@ def main():
                                  row_block=ROW_BLOCK, rank=rank, nranks=nr, device=local_rank,
                                  accel=accel)
         if nr > 1:
-            tiles.gather(tile, gathered)  # RCCL all-gather over xGMI
+            if backend == "nccl":
+                tiles.gather(tile, gathered)  # RCCL all-gather over xGMI
+            else:
+                gathered.copy_(tiles.gather_any(tile.cpu(), nr))
         return st
 
     for _ in range(args.warmup):
@@ -145,10 +156,19 @@ def main():
     rays = sum(s["rays"] for s in stats)
     trace_ms = sum(s["trace_ms"] for s in stats) / max(1, sum(s["trace_launches"] for s in stats))
     if nr > 1:
-        t = torch.tensor([elapsed, float(rays)], dtype=torch.float64, device=dev)
-        dist.all_reduce(t[:1], op=dist.ReduceOp.MAX)
-        dist.all_reduce(t[1:], op=dist.ReduceOp.SUM)
-        elapsed, rays = float(t[0]), int(t[1])
+        tdev = dev if backend == "nccl" else torch.device("cpu")
+        t_max = torch.tensor([elapsed], dtype=torch.float64, device=tdev)
+        t_sum = torch.tensor([float(rays)], dtype=torch.float64, device=tdev)
+        dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
+        dist.all_reduce(t_sum, op=dist.ReduceOp.SUM)
+        elapsed, rays = float(t_max[0]), int(t_sum[0])
+        if os.environ.get("RT_BENCH_VERIFY") == "1":
+            # the assembled frame must equal a one-rank render (rehearsal check)
+            img = tiles.assemble(gathered.cpu().numpy(), W, H, ROW_BLOCK, nr)
+            if rank == 0:
+                ref, _ = world.render(W, H, spp, depth, accel=accel, device=local_rank)
+                assert (img == ref).all(), "assembled multi-rank frame differs"
+                print("verify: assembled frame == single-rank frame", file=sys.stderr)
     if rank != 0:
         dist.destroy_process_group()
         return
