@@ -55,7 +55,7 @@ Rust_WorldHandle *load_world(const char *source) {
     const char *tleaf = std::getenv("RT_AMD_TRI_LEAF");  // triangles per BVH leaf
     world->state.tbvh = rtamd::build_triangle_bvh(world->state.scene.triangles,
                                                   world->state.packed.tri_hot,
-                                                  tleaf ? (uint32_t)std::atoi(tleaf) : 4u);
+                                                  tleaf ? (uint32_t)std::atoi(tleaf) : 2u);
     // bounce-0 triangle tree for the scene camera (rebuilt by the first render
     // after move_camera_position, which does not see the world)
     rtamd::prepare_camera(world->state, world->state.scene.camera);

@@ -182,7 +182,7 @@ void prepare_camera(WorldState &w, const CameraModel &cam) {
     if (w.tbvh.nodes.empty() || env_u64("RT_AMD_CAMERA_TREE", 1) == 0) return;
     const float o[3] = {cam.origin.x, cam.origin.y, cam.origin.z};
     if (w.ctree_version && std::memcmp(o, w.ctree.origin, sizeof(o)) == 0) return;
-    const uint64_t leaf = env_u64("RT_AMD_TRI_LEAF", 4);
+    const uint64_t leaf = env_u64("RT_AMD_CAM_LEAF", 2);  // triangles per camera-tree leaf
     w.ctree = build_camera_triangle_bvh(w.scene.triangles, w.packed.tri_hot, w.tbvh, o,
                                         (uint32_t)leaf);
     ++w.ctree_version;
@@ -224,7 +224,7 @@ int render_frame(WorldState &w, const CameraModel &cam, size_t width, size_t hei
     const uint32_t spp = o.samples_per_pixel > 0 ? (uint32_t)o.samples_per_pixel : 0u;
     const uint64_t jobs_per_row = (uint64_t)width * spp;
     if (jobs_per_row > 0x7FFFFFFFull) { set_error("width*spp too large"); return -1; }
-    const uint64_t slab_jobs = env_u64("RT_AMD_SLAB_JOBS", 1ull << 28);
+    const uint64_t slab_jobs = env_u64("RT_AMD_SLAB_JOBS", 1ull << 30);  // 16 GB of slab at most
     size_t rows_per_slab = jobs_per_row ? (size_t)std::max<uint64_t>(1, slab_jobs / jobs_per_row) : T;
     rows_per_slab = std::min(rows_per_slab, T);
     if (jobs_per_row) HIP_TRY(grow(d->samples, d->samples_cap, rows_per_slab * jobs_per_row));

@@ -211,8 +211,8 @@ def test_slabs_do_not_change_the_frame(monkeypatch):
 
 @pytest.mark.parametrize("scene", ["rtow", "mesh_soup"])
 def test_scheduling_knobs_do_not_change_samples(monkeypatch, scene):
-    """Job-queue partitions, chunk size and walk slicing only reorder work:
-    every sample colour must be identical."""
+    """Job-queue partitions, chunk size, walk slicing, the tree's memory (LDS
+    or global) and the inflation bound only change work, never a sample."""
     src = scene_text("rtow.txt") if scene == "rtow" else _triangle_scene(41, 400, spheres=40)
     w, h, spp = 160, 90, 4
     world = R.World(src)
@@ -221,7 +221,9 @@ def test_scheduling_knobs_do_not_change_samples(monkeypatch, scene):
     for env in [dict(RT_AMD_PARTS="1"), dict(RT_AMD_PARTS="7", RT_AMD_CHUNK="64"),
                 dict(RT_AMD_PARTS="1024"), dict(RT_AMD_STEP="1", RT_AMD_STEPS="1"),
                 dict(RT_AMD_STEP="1", RT_AMD_STEPS="5"), dict(RT_AMD_STEP="0"),
-                dict(RT_AMD_REFILL="17")]:
+                dict(RT_AMD_REFILL="17"), dict(RT_AMD_LDS="0"),
+                dict(RT_AMD_LDS="0", RT_AMD_STEP="1", RT_AMD_STEPS="3"),
+                dict(RT_AMD_LINEAR_E="1")]:
         for k, v in env.items():
             monkeypatch.setenv(k, v)
         out, _ = world.render(w, h, spp, 8)
