@@ -276,6 +276,79 @@ static std::vector<float> triangle_records(const std::vector<Prim> &prims,
     return out;
 }
 
+// ---- quantised kernel nodes (bvh.h QuantGrid)
+static float qdec(uint32_t q, float step, float base) { return std::fmaf((float)q, step, base); }
+
+// grid over [lo, hi] with 65535 steps whose decode covers both ends
+static void make_grid(float lo, float hi, float &base, float &step) {
+    base = lo;
+    step = hi > lo ? up(((double)hi - (double)lo) / 65535.0 * (1 + 1e-6))
+                   : std::numeric_limits<float>::min();
+    while (qdec(65535, step, base) < hi) step = std::nextafter(step, std::numeric_limits<float>::infinity());
+}
+static uint32_t q_down(float x, float step, float base) {  // largest q: decode(q) <= x
+    double g = std::floor(((double)x - base) / step);
+    uint32_t q = (uint32_t)std::min(65535.0, std::max(0.0, g));
+    while (q > 0 && qdec(q, step, base) > x) --q;
+    while (q < 65535 && qdec(q + 1, step, base) <= x) ++q;
+    return q;
+}
+static uint32_t q_up(float x, float step, float base) {  // smallest q: decode(q) >= x
+    double g = std::ceil(((double)x - base) / step);
+    uint32_t q = (uint32_t)std::min(65535.0, std::max(0.0, g));
+    while (q < 65535 && qdec(q, step, base) < x) ++q;
+    while (q > 0 && qdec(q - 1, step, base) >= x) --q;
+    return q;
+}
+static uint32_t node_word(const float *lo_a, const float *hi_b) {  // a, b bits -> kernel a
+    uint32_t a, b;
+    std::memcpy(&a, lo_a, 4);
+    std::memcpy(&b, hi_b, 4);
+    if (a & kLeafBit) return kLeafBit | ((a & ~kLeafBit) << 3) | b;  // first << 3 | count
+    return a | (b << 29);                                             // child | axis << 29
+}
+// nodes: `stride` floats per node (min.xyz, a) (max.xyz, b) [(nmin) (nmax)]
+static void quantize_boxes(const std::vector<float> &nodes, size_t stride, bool normals,
+                           std::vector<uint32_t> &q, QuantGrid &g, float *nbase, float *nstep) {
+    const size_t n = nodes.size() / stride;
+    float lo[3], hi[3], nlo = 1, nhi = -1;
+    for (int k = 0; k < 3; ++k) { lo[k] = nodes[k]; hi[k] = nodes[4 + k]; }  // root holds all
+    for (size_t i = 0; i < n && normals; ++i)
+        for (int k = 0; k < 3; ++k) {
+            nlo = std::min(nlo, nodes[i * stride + 8 + k]);
+            nhi = std::max(nhi, nodes[i * stride + 12 + k]);
+        }
+    for (int k = 0; k < 3; ++k) make_grid(lo[k], hi[k], g.base[k], g.step[k]);
+    if (normals) make_grid(nlo, nhi, *nbase, *nstep);
+    const size_t words = normals ? 8 : 4;
+    q.assign(n * words, 0);
+    for (size_t i = 0; i < n; ++i) {
+        const float *f = &nodes[i * stride];
+        uint32_t b[6];
+        for (int k = 0; k < 3; ++k) {
+            b[k] = q_down(f[k], g.step[k], g.base[k]);
+            b[3 + k] = q_up(f[4 + k], g.step[k], g.base[k]);
+        }
+        uint32_t *w = &q[i * words];
+        w[0] = b[0] | b[1] << 16;
+        w[1] = b[2] | b[3] << 16;
+        w[2] = b[4] | b[5] << 16;
+        if (normals) {
+            uint32_t m[6];
+            for (int k = 0; k < 3; ++k) {
+                m[k] = q_down(f[8 + k], *nstep, *nbase);
+                m[3 + k] = q_up(f[12 + k], *nstep, *nbase);
+            }
+            w[3] = m[0] | m[1] << 16;
+            w[4] = m[2] | m[3] << 16;
+            w[5] = m[4] | m[5] << 16;
+            w[6] = node_word(&f[3], &f[7]);
+        } else {
+            w[3] = node_word(&f[3], &f[7]);
+        }
+    }
+}
+
 TriangleBVH build_triangle_bvh(const std::vector<Triangle> &tris, const std::vector<float> &tri_hot,
                                uint32_t leaf_size, const float *oc, double phantom) {
     TriangleBVH out;
@@ -299,7 +372,9 @@ TriangleBVH build_triangle_bvh(const std::vector<Triangle> &tris, const std::vec
         }
         prims.push_back(p);
     }
-    if (prims.size() < 16) {  // not worth a tree: brute force keeps the reference order
+    if (prims.size() < 16 || prims.size() >= (1u << 27)) {
+        // not worth a tree (brute force keeps the reference order), or beyond the
+        // kernel node encoding (first < 2^28, child < 2^29)
         out.loose.clear();
         return out;
     }
@@ -315,7 +390,7 @@ TriangleBVH build_triangle_bvh(const std::vector<Triangle> &tris, const std::vec
     double L = 0.4 * (std::sqrt(cn) + hd / 2);  // A/B on C5 (tools/tbvh_sim.cpp): 1-4 best
     if (const char *e = std::getenv("RT_AMD_TRI_PHANTOM")) L = std::atof(e);
     if (phantom > 0) L = phantom;
-    Builder b(prims, std::max(1u, leaf_size), L > 0 ? L : 1e-30);
+    Builder b(prims, std::min(7u, std::max(1u, leaf_size)), L > 0 ? L : 1e-30);  // count: 3 bits
     b.nodes.reserve(prims.size() * 2);
     b.nodes.emplace_back();
     b.build(0, 0, (uint32_t)prims.size(), 0);
@@ -354,6 +429,7 @@ TriangleBVH build_triangle_bvh(const std::vector<Triangle> &tris, const std::vec
     out.miss.assign(b.nodes.size() * 8, kNodeEnd);
     for (uint32_t oct = 0; oct < 8; ++oct) b.links(0, kNodeEnd, oct, out.miss);
     out.tris = triangle_records(prims, tris, tri_hot);
+    quantize_boxes(out.nodes, 16, true, out.qnodes, out.qbox, &out.nbase, &out.nstep);
     return out;
 }
 
@@ -384,7 +460,7 @@ CameraTriangleBVH build_camera_triangle_bvh(const std::vector<Triangle> &tris,
         prims.push_back(p);
     }
     if (prims.empty()) return out;
-    Builder b(prims, std::max(1u, leaf_size));
+    Builder b(prims, std::min(7u, std::max(1u, leaf_size)));  // count: 3 bits
     b.nodes.reserve(prims.size() * 2);
     b.nodes.emplace_back();
     b.build(0, 0, (uint32_t)prims.size(), 0);
@@ -400,6 +476,7 @@ CameraTriangleBVH build_camera_triangle_bvh(const std::vector<Triangle> &tris,
     out.miss.assign(b.nodes.size() * 8, kNodeEnd);
     for (uint32_t oct = 0; oct < 8; ++oct) b.links(0, kNodeEnd, oct, out.miss);
     out.tris = triangle_records(prims, tris, tri_hot);
+    quantize_boxes(out.nodes, 8, false, out.qnodes, out.qbox, nullptr, nullptr);
     return out;
 }
 

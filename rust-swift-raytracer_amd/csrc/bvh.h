@@ -49,6 +49,13 @@ SphereBVH build_sphere_bvh(const std::vector<Sphere> &spheres, uint32_t leaf_siz
 // 2(n^.o)n^ over that normal box plus a rounding margin.
 // Nodes: four float4 -- (min.xyz, a) (max.xyz, b) (nmin.xyz, 0) (nmax.xyz, 0)
 // with a/b as in SphereBVH.
+// Kernel image of a triangle tree's boxes: u16 per coordinate on a per-tree
+// grid, decoded as fmaf(q, step, base); lower faces round down and upper faces
+// up, so a decoded box always contains the float box (checked by decoding).
+struct QuantGrid {
+    float base[3] = {0, 0, 0}, step[3] = {1, 1, 1};
+};
+
 struct TriangleBVH {
     std::vector<float> nodes;       // 16 floats per node
     std::vector<uint32_t> miss;     // 8 per node
@@ -62,6 +69,11 @@ struct TriangleBVH {
     // 2(n^.d)n^ with d = o - oc (oc = 0: the plain tree).
     float oc[3] = {0, 0, 0};
     uint32_t depth = 0;
+    // kernel nodes, 8 u32: box (6 x u16), normal box (6 x u16), a, 0 with
+    // a = child | axis << 29 (internal) or 1 << 31 | first << 3 | count (leaf)
+    std::vector<uint32_t> qnodes;
+    QuantGrid qbox;
+    float nbase = -1, nstep = 1;    // normal grid (all three axes)
 };
 
 // tri_hot: PackedScene::tri_hot (the exact per-triangle n and n.v0 bits).
@@ -83,6 +95,8 @@ struct CameraTriangleBVH {
     std::vector<float> tris;
     float origin[3] = {0, 0, 0};
     uint32_t depth = 0;
+    std::vector<uint32_t> qnodes;   // kernel nodes, 4 u32: box (6 x u16), a (as TriangleBVH)
+    QuantGrid qbox;
 };
 CameraTriangleBVH build_camera_triangle_bvh(const std::vector<Triangle> &tris,
                                             const std::vector<float> &tri_hot, const TriangleBVH &tb,

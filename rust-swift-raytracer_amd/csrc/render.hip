@@ -373,13 +373,38 @@ __device__ __forceinline__ void tri_node(const TraceParams &p, F3 org, F3 inv, F
                                          bool cam, float rho, float cap, uint32_t &node,
                                          uint32_t &leaf, uint32_t &node_tests) {
     ++node_tests;
-    const float4 *nodes = cam ? p.cam_nodes : p.tbvh_nodes;
+    // Quantised nodes (bvh.h QuantGrid): u16 coordinates decoded with one fma
+    // on the tree's grid; the host rounds every face outward *after* this
+    // exact decode, so a decoded box contains the float box.
     const uint32_t *links = cam ? p.cam_miss : p.tbvh_miss;
-    const float4 *nd = nodes + (cam ? 2u : 4u) * node;
-    const float4 B0 = nd[0], B1 = nd[1];
-    float4 N0 = make_float4(0.0f, 0.0f, 0.0f, 0.0f), N1 = N0;  // camera tree: no widening
-    if (!cam) { N0 = nd[2]; N1 = nd[3]; }
+    uint4 q0, q1 = make_uint4(0u, 0u, 0u, 0u);
+    uint32_t a;
+    if (cam) {
+        q0 = p.cam_nodes[node];
+        a = q0.w;
+    } else {
+        q0 = p.tbvh_nodes[2u * node];
+        q1 = p.tbvh_nodes[2u * node + 1u];
+        a = q1.z;
+    }
     const uint32_t miss = links[8u * node + oct];
+    const float gbx = cam ? p.cq_base[0] : p.tq_base[0], gsx = cam ? p.cq_step[0] : p.tq_step[0];
+    const float gby = cam ? p.cq_base[1] : p.tq_base[1], gsy = cam ? p.cq_step[1] : p.tq_step[1];
+    const float gbz = cam ? p.cq_base[2] : p.tq_base[2], gsz = cam ? p.cq_step[2] : p.tq_step[2];
+    auto lo16 = [](uint32_t w) { return (float)(w & 0xFFFFu); };
+    auto hi16 = [](uint32_t w) { return (float)(w >> 16); };
+    const float4 B0 = make_float4(__builtin_fmaf(lo16(q0.x), gsx, gbx), __builtin_fmaf(hi16(q0.x), gsy, gby),
+                                  __builtin_fmaf(lo16(q0.y), gsz, gbz), 0.0f);
+    const float4 B1 = make_float4(__builtin_fmaf(hi16(q0.y), gsx, gbx), __builtin_fmaf(lo16(q0.z), gsy, gby),
+                                  __builtin_fmaf(hi16(q0.z), gsz, gbz), 0.0f);
+    float4 N0 = make_float4(0.0f, 0.0f, 0.0f, 0.0f), N1 = N0;  // camera tree: no widening
+    if (!cam) {
+        const float nb = p.tq_nbase, ns = p.tq_nstep;
+        N0 = make_float4(__builtin_fmaf(lo16(q0.w), ns, nb), __builtin_fmaf(hi16(q0.w), ns, nb),
+                         __builtin_fmaf(lo16(q1.x), ns, nb), 0.0f);
+        N1 = make_float4(__builtin_fmaf(hi16(q1.x), ns, nb), __builtin_fmaf(lo16(q1.y), ns, nb),
+                         __builtin_fmaf(hi16(q1.y), ns, nb), 0.0f);
+    }
     // s = n^.d over the normal box, d = o - oc (the tree's box origin, bvh.h)
     const float ax = N0.x * dlt.x, bx = N1.x * dlt.x;
     const float ay = N0.y * dlt.y, by = N1.y * dlt.y;
@@ -403,11 +428,11 @@ __device__ __forceinline__ void tri_node(const TraceParams &p, F3 org, F3 inv, F
     const float tn = fmaxf(fmaxf(fminf(t0x, t1x), fminf(t0y, t1y)), fminf(t0z, t1z));
     const float tf = fminf(fminf(fmaxf(t0x, t1x), fmaxf(t0y, t1y)), fmaxf(t0z, t1z));
     const bool skip = tn > tf || tf < 0.001f || tn > cap;
-    const uint32_t a = __float_as_uint(B0.w);
+    // a: child | axis << 29, or leaf bit | first << 3 | count
     const bool is_leaf = (a & kLeafBitDev) != 0;
-    const uint32_t child = a + ((oct >> __float_as_uint(B1.w)) & 1u);
+    const uint32_t child = (a & 0x1FFFFFFFu) + ((oct >> (a >> 29)) & 1u);
     node = (skip || is_leaf) ? miss : child;
-    if (!skip && is_leaf) leaf = ((a & ~kLeafBitDev) << 3) | __float_as_uint(B1.w);
+    if (!skip && is_leaf) leaf = a & ~kLeafBitDev;
 }
 
 __device__ __forceinline__ void tri_leaf(const TraceParams &p, F3 org, F3 dir, bool cam,

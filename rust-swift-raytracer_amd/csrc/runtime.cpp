@@ -156,11 +156,11 @@ static int device_for(WorldState &w, int want, DeviceState *&out) {
                 if (e != hipSuccess || src.empty()) return e;
                 return hipMemcpy(*dst, src.data(), src.size() * sizeof(uint32_t), hipMemcpyHostToDevice);
             };
-            HIP_TRY(up((void **)&d->tbvh_nodes, tb.nodes));
+            HIP_TRY(upu((void **)&d->tbvh_nodes, tb.qnodes));
             HIP_TRY(up((void **)&d->tbvh_tris, tb.tris));
             HIP_TRY(upu((void **)&d->tbvh_miss, tb.miss));
             HIP_TRY(upu((void **)&d->tbvh_loose, tb.loose));
-            d->tnodes = (uint32_t)(tb.nodes.size() / 16);
+            d->tnodes = (uint32_t)(tb.qnodes.size() / 8);
             d->ttris = (uint32_t)(tb.tris.size() / 16);
             d->tloose = (uint32_t)tb.loose.size();
         }
@@ -279,18 +279,19 @@ int render_frame(WorldState &w, const CameraModel &cam, size_t width, size_t hei
     if (use_tbvh && w.ctree_version && d->cam_version != w.ctree_version) {
         for (void *b : {(void *)d->cam_nodes, (void *)d->cam_tris, (void *)d->cam_miss})
             if (b) HIP_TRY(hipFree(b));
-        d->cam_nodes = d->cam_tris = nullptr;
+        d->cam_nodes = nullptr;
+        d->cam_tris = nullptr;
         d->cam_miss = nullptr;
         d->cam_nnodes = 0;
         const CameraTriangleBVH &ct = w.ctree;
         if (!ct.nodes.empty()) {
-            HIP_TRY(hipMalloc((void **)&d->cam_nodes, ct.nodes.size() * 4));
-            HIP_TRY(hipMemcpy(d->cam_nodes, ct.nodes.data(), ct.nodes.size() * 4, hipMemcpyHostToDevice));
+            HIP_TRY(hipMalloc((void **)&d->cam_nodes, ct.qnodes.size() * 4));
+            HIP_TRY(hipMemcpy(d->cam_nodes, ct.qnodes.data(), ct.qnodes.size() * 4, hipMemcpyHostToDevice));
             HIP_TRY(hipMalloc((void **)&d->cam_tris, ct.tris.size() * 4));
             HIP_TRY(hipMemcpy(d->cam_tris, ct.tris.data(), ct.tris.size() * 4, hipMemcpyHostToDevice));
             HIP_TRY(hipMalloc((void **)&d->cam_miss, ct.miss.size() * 4));
             HIP_TRY(hipMemcpy(d->cam_miss, ct.miss.data(), ct.miss.size() * 4, hipMemcpyHostToDevice));
-            d->cam_nnodes = (uint32_t)(ct.nodes.size() / 8);
+            d->cam_nnodes = (uint32_t)(ct.qnodes.size() / 4);
         }
         d->cam_version = w.ctree_version;
     }
@@ -298,12 +299,20 @@ int render_frame(WorldState &w, const CameraModel &cam, size_t width, size_t hei
         if (d->cam_nnodes && std::memcmp(w.ctree.origin, &cam.origin, 12) == 0) {
             p.cam_nodes = d->cam_nodes; p.cam_miss = d->cam_miss; p.cam_tris = d->cam_tris;
             p.cam_nnodes = d->cam_nnodes;
+            for (int k = 0; k < 3; ++k) { p.cq_base[k] = w.ctree.qbox.base[k]; p.cq_step[k] = w.ctree.qbox.step[k]; }
         }
         const TriangleBVH &tb = w.tbvh;
         p.tbvh_nodes = d->tbvh_nodes; p.tbvh_miss = d->tbvh_miss;
         p.tbvh_tris = d->tbvh_tris; p.tbvh_loose = d->tbvh_loose;
         p.tnodes = d->tnodes; p.ttris = d->ttris; p.tloose = d->tloose;
-        for (int k = 0; k < 3; ++k) { p.tbvh_c[k] = tb.centre[k]; p.tbvh_oc[k] = tb.oc[k]; }
+        for (int k = 0; k < 3; ++k) {
+            p.tbvh_c[k] = tb.centre[k];
+            p.tbvh_oc[k] = tb.oc[k];
+            p.tq_base[k] = tb.qbox.base[k];
+            p.tq_step[k] = tb.qbox.step[k];
+        }
+        p.tq_nbase = tb.nbase;
+        p.tq_nstep = tb.nstep;
         p.tbvh_r = tb.radius; p.tbvh_mag = tb.mag;
     }
     const float inv_spp = 1.0f / (float)o.samples_per_pixel;  // 1.0 / spp as f32 (common.rs:345)

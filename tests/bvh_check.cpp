@@ -1,0 +1,151 @@
+// bvh_check.cpp -- host-side structural checks of the BVH builders (CPU test
+// driver for tests/test_bvh_host.py; compiled with g++ against csrc/bvh.cpp).
+// Checks, for the sphere tree, the static triangle tree and the camera tree:
+//   * every primitive sits in exactly one leaf, leaves within limits;
+//   * every node's float box contains its children's boxes and its prims;
+//   * octant links: each link is a valid node index or the end marker, and a
+//     full walk entering every node visits each node exactly once per octant;
+//   * quantised kernel nodes decode (fmaf(q, step, base)) to boxes containing
+//     the float boxes, and the packed child/axis/leaf words round-trip.
+// Prints "OK <counts>" or the first failure and exits non-zero.
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <fstream>
+#include <sstream>
+#include <vector>
+
+#include "bvh.h"
+#include "scene.h"
+
+using namespace rtamd;
+
+static int fails = 0;
+#define CHECK(c, ...)                                   \
+    do {                                                \
+        if (!(c)) {                                     \
+            if (fails++ < 10) std::printf(__VA_ARGS__); \
+        }                                               \
+    } while (0)
+
+static uint32_t bits(float f) { uint32_t u; std::memcpy(&u, &f, 4); return u; }
+
+// nodes: stride floats, (min, a) (max, b); walk with links, every node entered
+static void check_links(const std::vector<float> &nodes, size_t stride, const std::vector<uint32_t> &miss,
+                        const char *what) {
+    const size_t n = nodes.size() / stride;
+    for (uint32_t oct = 0; oct < 8; ++oct) {
+        std::vector<int> seen(n, 0);
+        uint32_t node = 0;
+        size_t steps = 0;
+        while (node != kNodeEnd && steps++ <= n) {
+            CHECK(node < n, "%s: link out of range\n", what);
+            if (node >= n) return;
+            seen[node]++;
+            const uint32_t a = bits(nodes[node * stride + 3]), b = bits(nodes[node * stride + 7]);
+            node = (a & kLeafBit) ? miss[node * 8 + oct] : a + ((oct >> b) & 1u);
+        }
+        for (size_t i = 0; i < n; ++i) CHECK(seen[i] == 1, "%s: node %zu seen %d times (oct %u)\n", what, i, seen[i], oct);
+    }
+}
+
+static void check_tree(const std::vector<float> &nodes, size_t stride, size_t nprims, uint32_t maxleaf,
+                       const char *what) {
+    const size_t n = nodes.size() / stride;
+    std::vector<int> owner(nprims, 0);
+    for (size_t i = 0; i < n; ++i) {
+        const float *f = &nodes[i * stride];
+        const uint32_t a = bits(f[3]), b = bits(f[7]);
+        for (int k = 0; k < 3; ++k) CHECK(f[k] <= f[4 + k], "%s: node %zu inverted box\n", what, i);
+        if (a & kLeafBit) {
+            const uint32_t first = a & ~kLeafBit;
+            CHECK(b >= 1 && b <= maxleaf, "%s: leaf %zu count %u\n", what, i, b);
+            for (uint32_t j = first; j < first + b && j < nprims; ++j) owner[j]++;
+        } else {
+            CHECK(a + 1 < n && b < 3, "%s: node %zu child %u axis %u\n", what, i, a, b);
+            for (uint32_t c = a; c <= a + 1 && c + 1 <= n; ++c)
+                for (int k = 0; k < 3; ++k) {
+                    CHECK(nodes[c * stride + k] >= f[k] && nodes[c * stride + 4 + k] <= f[4 + k],
+                          "%s: child %u box not inside parent %zu\n", what, c, i);
+                    if (stride == 16)
+                        CHECK(nodes[c * stride + 8 + k] >= f[8 + k] && nodes[c * stride + 12 + k] <= f[12 + k],
+                              "%s: child %u normal box not inside parent %zu\n", what, c, i);
+                }
+        }
+    }
+    for (size_t j = 0; j < nprims; ++j) CHECK(owner[j] == 1, "%s: prim %zu in %d leaves\n", what, j, owner[j]);
+}
+
+static void check_quant(const std::vector<float> &nodes, size_t stride, const std::vector<uint32_t> &q,
+                        const QuantGrid &g, float nb, float ns, const char *what) {
+    const size_t n = nodes.size() / stride, words = stride == 16 ? 8 : 4;
+    CHECK(q.size() == n * words, "%s: qnodes size\n", what);
+    auto dec = [](uint32_t v, float s, float b) { return std::fmaf((float)v, s, b); };
+    for (size_t i = 0; i < n && q.size() == n * words; ++i) {
+        const float *f = &nodes[i * stride];
+        const uint32_t *w = &q[i * words];
+        const uint32_t u[6] = {w[0] & 0xFFFF, w[0] >> 16, w[1] & 0xFFFF, w[1] >> 16, w[2] & 0xFFFF, w[2] >> 16};
+        for (int k = 0; k < 3; ++k) {
+            CHECK(dec(u[k], g.step[k], g.base[k]) <= f[k], "%s: node %zu lo %d not conservative\n", what, i, k);
+            CHECK(dec(u[3 + k], g.step[k], g.base[k]) >= f[4 + k], "%s: node %zu hi %d not conservative\n", what, i, k);
+            // and tight: within 2 grid steps
+            CHECK(f[k] - dec(u[k], g.step[k], g.base[k]) <= 2 * g.step[k], "%s: node %zu lo %d loose\n", what, i, k);
+        }
+        if (stride == 16) {
+            const uint32_t m[6] = {w[3] & 0xFFFF, w[3] >> 16, w[4] & 0xFFFF, w[4] >> 16, w[5] & 0xFFFF, w[5] >> 16};
+            for (int k = 0; k < 3; ++k) {
+                CHECK(dec(m[k], ns, nb) <= f[8 + k], "%s: node %zu nlo %d\n", what, i, k);
+                CHECK(dec(m[3 + k], ns, nb) >= f[12 + k], "%s: node %zu nhi %d\n", what, i, k);
+            }
+        }
+        const uint32_t a = bits(f[3]), b = bits(f[7]), word = w[words == 8 ? 6 : 3];
+        if (a & kLeafBit)
+            CHECK(word == (kLeafBit | ((a & ~kLeafBit) << 3) | b), "%s: leaf word %zu\n", what, i);
+        else
+            CHECK((word & 0x1FFFFFFFu) == a && (word >> 29) == b, "%s: internal word %zu\n", what, i);
+    }
+}
+
+int main(int argc, char **argv) {
+    std::ifstream fh(argv[1]);
+    std::stringstream ss;
+    ss << fh.rdbuf();
+    SceneModel s;
+    if (parse_scene(ss.str(), s) != kParseOk) { std::printf("parse error\n"); return 2; }
+    PackedScene p = pack_scene(s, 8, 1);
+    const uint32_t leaf = argc > 2 ? (uint32_t)std::atoi(argv[2]) : 2;
+    SphereBVH sb = build_sphere_bvh(s.spheres, 3);
+    if (!sb.nodes.empty()) {
+        check_tree(sb.nodes, 8, sb.prim_id.size(), 3, "sphere");
+        check_links(sb.nodes, 8, sb.miss, "sphere");
+    }
+    TriangleBVH tb = build_triangle_bvh(s.triangles, p.tri_hot, leaf);
+    CameraTriangleBVH cb;
+    if (!tb.nodes.empty()) {
+        check_tree(tb.nodes, 16, tb.tris.size() / 16, leaf, "static");
+        check_links(tb.nodes, 16, tb.miss, "static");
+        check_quant(tb.nodes, 16, tb.qnodes, tb.qbox, tb.nbase, tb.nstep, "static");
+        const float o[3] = {s.camera.origin.x, s.camera.origin.y, s.camera.origin.z};
+        cb = build_camera_triangle_bvh(s.triangles, p.tri_hot, tb, o, leaf);
+        check_tree(cb.nodes, 8, cb.tris.size() / 16, leaf, "camera");
+        check_links(cb.nodes, 8, cb.miss, "camera");
+        check_quant(cb.nodes, 8, cb.qnodes, cb.qbox, 0, 1, "camera");
+        CHECK(cb.tris.size() == tb.tris.size(), "camera tree holds %zu records, static %zu\n",
+              cb.tris.size() / 16, tb.tris.size() / 16);
+    }
+    // every triangle is in the tree, brute-forced (loose) or degenerate (n = 0)
+    size_t in_tree = tb.tris.size() / 16, degenerate = 0;
+    for (size_t i = 0; i < s.triangles.size(); ++i) {
+        const float *h = &p.tri_hot[i * 4];
+        if (h[0] == 0 && h[1] == 0 && h[2] == 0) ++degenerate;
+    }
+    if (!tb.nodes.empty())
+        CHECK(in_tree + tb.loose.size() + degenerate >= s.triangles.size(),
+              "triangles lost: %zu tree + %zu loose + %zu degenerate < %zu\n", in_tree, tb.loose.size(),
+              degenerate, s.triangles.size());
+    if (fails) return 1;
+    std::printf("OK spheres %zu nodes %zu | triangles %zu tree %zu loose %zu nodes %zu camera nodes %zu\n",
+                s.spheres.size(), sb.nodes.size() / 8, s.triangles.size(), in_tree, tb.loose.size(),
+                tb.nodes.size() / 16, cb.nodes.size() / 8);
+    return 0;
+}

@@ -322,48 +322,7 @@ def test_bvh_full_size_c2_equals_brute_force():
 
 
 # ------------------------------------------------------- exact triangle BVH
-def _triangle_scene(seed, n, spread=4.0, size=0.5, cam=(0.0, 0.0, 0.0), offset=(0.0, 0.0, 0.0),
-                    slivers=0, dup=0, spheres=0, big=0, grid=0):
-    """Random triangle soup (+ optional spheres) in the scene DSL.  Mixes
-    sizes and orientations, near-degenerate slivers, exact duplicates (equal t:
-    the lower index must win), huge triangles and a coplanar grid."""
-    rng = np.random.default_rng(seed)
-    kinds = ["Diffuse color 0.7 0.5 0.3", "Metal color 0.9 0.8 0.7 fuzz 0.05",
-             "Dielectric ir 1.5", "Metal color 0.6 0.6 0.9 fuzz 0.0"]
-    lines = [f"camera origin {cam[0]:.6f} {cam[1]:.6f} {cam[2]:.6f} aspect 1.5;"]
-    lines += [f"material K{i} : {k};" for i, k in enumerate(kinds)]
-    off = np.array(offset) + np.array([0.0, 0.0, -spread - 2.0])
-    tris = []
-    for _ in range(n):
-        c = rng.uniform(-spread, spread, 3) + off
-        e = rng.normal(size=(2, 3)) * size * rng.uniform(0.1, 1.0)
-        tris.append((c, c + e[0], c + e[1], int(rng.integers(0, 4))))
-    for _ in range(slivers):
-        c = rng.uniform(-spread, spread, 3) + off
-        d = rng.normal(size=3)
-        tris.append((c, c + d, c + 2.0 * d + rng.normal(size=3) * 1e-4, int(rng.integers(0, 4))))
-    for _ in range(big):
-        c = rng.uniform(-spread, spread, 3) + off
-        e = rng.normal(size=(2, 3)) * 40.0
-        tris.append((c, c + e[0], c + e[1], int(rng.integers(0, 4))))
-    for j in range(grid):
-        for i in range(grid):
-            x0, z0 = -3.0 + 6.0 * i / grid, -3.0 + 6.0 * j / grid
-            dx = 6.0 / grid
-            a = np.array([x0, -1.5, z0]) + off
-            b, c2, d = a + [dx, 0, 0], a + [0, 0, dx], a + [dx, 0, dx]
-            tris.append((a, c2, b, 0))
-            tris.append((b, c2, d, 1))
-    tris += tris[:dup]
-    for _ in range(spheres):  # the parser takes spheres before triangles only
-        c = rng.uniform(-spread, spread, 3) + off
-        lines.append(f"sphere center {c[0]:.6f} {c[1]:.6f} {c[2]:.6f} radius "
-                     f"{rng.uniform(0.1, 0.6):.6f} material K{int(rng.integers(0, 4))};")
-    for (v0, v1, v2, k) in tris:
-        lines.append("triangle v0 " + " ".join(f"{x:.6f}" for x in v0) + " v1 " +
-                     " ".join(f"{x:.6f}" for x in v1) + " v2 " +
-                     " ".join(f"{x:.6f}" for x in v2) + f" material K{k};")
-    return "\n".join(lines) + "\n"
+_triangle_scene = S.triangle_soup
 
 
 @pytest.mark.parametrize("case", [
