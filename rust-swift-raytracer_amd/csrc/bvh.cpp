@@ -307,9 +307,16 @@ static uint32_t node_word(const float *lo_a, const float *hi_b) {  // a, b bits 
     if (a & kLeafBit) return kLeafBit | ((a & ~kLeafBit) << 3) | b;  // first << 3 | count
     return a | (b << 29);                                             // child | axis << 29
 }
-// nodes: `stride` floats per node (min.xyz, a) (max.xyz, b) [(nmin) (nmax)]
+// nodes: `stride` floats per node (min.xyz, a) (max.xyz, b) [(nmin) (nmax)].
+// Kernel image, 8 u32 per node, one 32-B sector:
+//   static: box (3 words) | normal box (3 words) | a | link
+//   camera: box (3 words) | a | link | 0 0 0
+// link = the DFS successor of a fixed child-a-first order (octant 0 of
+// `miss`): octant-ordered links change node visits by 1-3 % at C5
+// (tools/tbvh_sim.cpp SIM_FIXED_OCT) but cost a second cache line per step.
 static void quantize_boxes(const std::vector<float> &nodes, size_t stride, bool normals,
-                           std::vector<uint32_t> &q, QuantGrid &g, float *nbase, float *nstep) {
+                           const std::vector<uint32_t> &miss, std::vector<uint32_t> &q, QuantGrid &g,
+                           float *nbase, float *nstep) {
     const size_t n = nodes.size() / stride;
     float lo[3], hi[3], nlo = 1, nhi = -1;
     for (int k = 0; k < 3; ++k) { lo[k] = nodes[k]; hi[k] = nodes[4 + k]; }  // root holds all
@@ -320,8 +327,7 @@ static void quantize_boxes(const std::vector<float> &nodes, size_t stride, bool 
         }
     for (int k = 0; k < 3; ++k) make_grid(lo[k], hi[k], g.base[k], g.step[k]);
     if (normals) make_grid(nlo, nhi, *nbase, *nstep);
-    const size_t words = normals ? 8 : 4;
-    q.assign(n * words, 0);
+    q.assign(n * 8, 0);
     for (size_t i = 0; i < n; ++i) {
         const float *f = &nodes[i * stride];
         uint32_t b[6];
@@ -329,7 +335,7 @@ static void quantize_boxes(const std::vector<float> &nodes, size_t stride, bool 
             b[k] = q_down(f[k], g.step[k], g.base[k]);
             b[3 + k] = q_up(f[4 + k], g.step[k], g.base[k]);
         }
-        uint32_t *w = &q[i * words];
+        uint32_t *w = &q[i * 8];
         w[0] = b[0] | b[1] << 16;
         w[1] = b[2] | b[3] << 16;
         w[2] = b[4] | b[5] << 16;
@@ -343,8 +349,10 @@ static void quantize_boxes(const std::vector<float> &nodes, size_t stride, bool 
             w[4] = m[2] | m[3] << 16;
             w[5] = m[4] | m[5] << 16;
             w[6] = node_word(&f[3], &f[7]);
+            w[7] = miss[i * 8];
         } else {
             w[3] = node_word(&f[3], &f[7]);
+            w[4] = miss[i * 8];
         }
     }
 }
@@ -429,7 +437,7 @@ TriangleBVH build_triangle_bvh(const std::vector<Triangle> &tris, const std::vec
     out.miss.assign(b.nodes.size() * 8, kNodeEnd);
     for (uint32_t oct = 0; oct < 8; ++oct) b.links(0, kNodeEnd, oct, out.miss);
     out.tris = triangle_records(prims, tris, tri_hot);
-    quantize_boxes(out.nodes, 16, true, out.qnodes, out.qbox, &out.nbase, &out.nstep);
+    quantize_boxes(out.nodes, 16, true, out.miss, out.qnodes, out.qbox, &out.nbase, &out.nstep);
     return out;
 }
 
@@ -476,7 +484,7 @@ CameraTriangleBVH build_camera_triangle_bvh(const std::vector<Triangle> &tris,
     out.miss.assign(b.nodes.size() * 8, kNodeEnd);
     for (uint32_t oct = 0; oct < 8; ++oct) b.links(0, kNodeEnd, oct, out.miss);
     out.tris = triangle_records(prims, tris, tri_hot);
-    quantize_boxes(out.nodes, 8, false, out.qnodes, out.qbox, nullptr, nullptr);
+    quantize_boxes(out.nodes, 8, false, out.miss, out.qnodes, out.qbox, nullptr, nullptr);
     return out;
 }
 

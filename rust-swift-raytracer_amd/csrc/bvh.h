@@ -69,8 +69,9 @@ struct TriangleBVH {
     // 2(n^.d)n^ with d = o - oc (oc = 0: the plain tree).
     float oc[3] = {0, 0, 0};
     uint32_t depth = 0;
-    // kernel nodes, 8 u32: box (6 x u16), normal box (6 x u16), a, 0 with
+    // kernel nodes, 8 u32: box (6 x u16), normal box (6 x u16), a, link with
     // a = child | axis << 29 (internal) or 1 << 31 | first << 3 | count (leaf)
+    // and link = miss[8 * node] (fixed child-a-first order)
     std::vector<uint32_t> qnodes;
     QuantGrid qbox;
     float nbase = -1, nstep = 1;    // normal grid (all three axes)
@@ -95,7 +96,7 @@ struct CameraTriangleBVH {
     std::vector<float> tris;
     float origin[3] = {0, 0, 0};
     uint32_t depth = 0;
-    std::vector<uint32_t> qnodes;   // kernel nodes, 4 u32: box (6 x u16), a (as TriangleBVH)
+    std::vector<uint32_t> qnodes;   // kernel nodes, 8 u32: box (6 x u16), a, link, 0 0 0
     QuantGrid qbox;
 };
 CameraTriangleBVH build_camera_triangle_bvh(const std::vector<Triangle> &tris,

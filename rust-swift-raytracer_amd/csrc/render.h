@@ -55,8 +55,7 @@ struct TraceParams {
     uint32_t step;            // ... when nonzero (else walks run to the end)
     float bvh_c[3], bvh_r, bvh_rmax, bvh_mag, bvh_inv_rmin;
     // phantom-aware triangle BVH (bvh.h TriangleBVH); tnodes == 0: brute-force Mesh loop
-    const uint4 *tbvh_nodes;  // 2 per node: quantised box, normal box, a (bvh.h TriangleBVH::qnodes)
-    const uint32_t *tbvh_miss;// 8 per node
+    const uint4 *tbvh_nodes;  // 2 per node: quantised box, normal box, a, link (bvh.h qnodes)
     const float4 *tbvh_tris;  // 4 per triangle in tree order: (n, n.v0) (v0, id) (v1) (v2)
     const uint32_t *tbvh_loose;  // triangles tested by brute force, ascending
     uint32_t tnodes, ttris, tloose;
@@ -66,8 +65,7 @@ struct TraceParams {
     float cq_base[3], cq_step[3];                      // camera-tree grid
     // the same triangles' phantoms for the camera origin (bvh.h CameraTriangleBVH),
     // used at bounce 0; cam_nnodes == 0: bounce 0 uses the tree above
-    const uint4 *cam_nodes;   // 1 per node: quantised box, a
-    const uint32_t *cam_miss; // 8 per node
+    const uint4 *cam_nodes;   // 2 per node: quantised box, a, link
     const float4 *cam_tris;   // 4 per triangle, as tbvh_tris
     uint32_t cam_nnodes;
 };

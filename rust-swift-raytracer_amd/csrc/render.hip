@@ -369,25 +369,19 @@ __device__ __forceinline__ bool tri_begin(const TraceParams &p, F3 org, F3 dir, 
 
 // One node of the triangle tree (static or camera-origin); an entered leaf is
 // handed back in `leaf` as (first << 3) | count, like sphere_node.
-__device__ __forceinline__ void tri_node(const TraceParams &p, F3 org, F3 inv, F3 dlt, uint32_t oct,
-                                         bool cam, float rho, float cap, uint32_t &node,
+__device__ __forceinline__ void tri_node(const TraceParams &p, F3 org, F3 inv, F3 dlt, bool cam,
+                                         float rho, float cap, uint32_t &node,
                                          uint32_t &leaf, uint32_t &node_tests) {
     ++node_tests;
     // Quantised nodes (bvh.h QuantGrid): u16 coordinates decoded with one fma
     // on the tree's grid; the host rounds every face outward *after* this
     // exact decode, so a decoded box contains the float box.
-    const uint32_t *links = cam ? p.cam_miss : p.tbvh_miss;
-    uint4 q0, q1 = make_uint4(0u, 0u, 0u, 0u);
-    uint32_t a;
-    if (cam) {
-        q0 = p.cam_nodes[node];
-        a = q0.w;
-    } else {
-        q0 = p.tbvh_nodes[2u * node];
-        q1 = p.tbvh_nodes[2u * node + 1u];
-        a = q1.z;
-    }
-    const uint32_t miss = links[8u * node + oct];
+    // one 32-B sector per node: (static) box | normals | a | link,
+    // (camera) box | a | link; fixed child-a-first order (bvh.cpp)
+    const uint4 *qn = (cam ? p.cam_nodes : p.tbvh_nodes) + 2u * node;
+    const uint4 q0 = qn[0], q1 = qn[1];
+    const uint32_t a = cam ? q0.w : q1.z;
+    const uint32_t miss = cam ? q1.x : q1.w;
     const float gbx = cam ? p.cq_base[0] : p.tq_base[0], gsx = cam ? p.cq_step[0] : p.tq_step[0];
     const float gby = cam ? p.cq_base[1] : p.tq_base[1], gsy = cam ? p.cq_step[1] : p.tq_step[1];
     const float gbz = cam ? p.cq_base[2] : p.tq_base[2], gsz = cam ? p.cq_step[2] : p.tq_step[2];
@@ -430,7 +424,7 @@ __device__ __forceinline__ void tri_node(const TraceParams &p, F3 org, F3 inv, F
     const bool skip = tn > tf || tf < 0.001f || tn > cap;
     // a: child | axis << 29, or leaf bit | first << 3 | count
     const bool is_leaf = (a & kLeafBitDev) != 0;
-    const uint32_t child = (a & 0x1FFFFFFFu) + ((oct >> (a >> 29)) & 1u);
+    const uint32_t child = a & 0x1FFFFFFFu;
     node = (skip || is_leaf) ? miss : child;
     if (!skip && is_leaf) leaf = a & ~kLeafBitDev;
 }
@@ -683,7 +677,7 @@ __attribute__((amdgpu_waves_per_eu(RT_WAVES_PER_EU, 8))) void trace_kernel(Trace
             const F3 dlt = f3(org.x - p.tbvh_oc[0], org.y - p.tbvh_oc[1], org.z - p.tbvh_oc[2]);
             do {
                 uint32_t leaf = 0;
-                tri_node(p, org, inv, dlt, oct, cam, e, fminf(best_t, tri_t), node, leaf, tnode_tests);
+                tri_node(p, org, inv, dlt, cam, e, fminf(best_t, tri_t), node, leaf, tnode_tests);
                 if (leaf != 0) tri_leaf(p, org, dir, cam, leaf, best_t, tri_t, tri_i, tri_in, tri_done);
             } while (node != kNodeEndDev && (!kStep || --budget != 0));
             if (node == kNodeEndDev) phase = kShade;

@@ -45,8 +45,8 @@ DeviceState::~DeviceState() {
     if (hipSetDevice(device) != hipSuccess) return;
     void *bufs[] = {sph_hot, sph_cold, tri_hot, tri_geo, mats, samples, out, replay, counter, stats,
                     bvh_nodes, bvh_prims, big_hot, bvh_miss, bvh_prim_id, big_id, bvh_miss16,
-                    sph_shade, sph_kind, tbvh_nodes, tbvh_tris, tbvh_miss, tbvh_loose,
-                    cam_nodes, cam_tris, cam_miss};
+                    sph_shade, sph_kind, tbvh_nodes, tbvh_tris, tbvh_loose,
+                    cam_nodes, cam_tris};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
     for (hipEvent_t e : ev)
@@ -158,7 +158,6 @@ static int device_for(WorldState &w, int want, DeviceState *&out) {
             };
             HIP_TRY(upu((void **)&d->tbvh_nodes, tb.qnodes));
             HIP_TRY(up((void **)&d->tbvh_tris, tb.tris));
-            HIP_TRY(upu((void **)&d->tbvh_miss, tb.miss));
             HIP_TRY(upu((void **)&d->tbvh_loose, tb.loose));
             d->tnodes = (uint32_t)(tb.qnodes.size() / 8);
             d->ttris = (uint32_t)(tb.tris.size() / 16);
@@ -277,11 +276,10 @@ int render_frame(WorldState &w, const CameraModel &cam, size_t width, size_t hei
     const bool use_tbvh = d->tnodes > 0 && o.accel != RT_ACCEL_BRUTE;
     if (use_tbvh) prepare_camera(w, cam);
     if (use_tbvh && w.ctree_version && d->cam_version != w.ctree_version) {
-        for (void *b : {(void *)d->cam_nodes, (void *)d->cam_tris, (void *)d->cam_miss})
+        for (void *b : {(void *)d->cam_nodes, (void *)d->cam_tris})
             if (b) HIP_TRY(hipFree(b));
         d->cam_nodes = nullptr;
         d->cam_tris = nullptr;
-        d->cam_miss = nullptr;
         d->cam_nnodes = 0;
         const CameraTriangleBVH &ct = w.ctree;
         if (!ct.nodes.empty()) {
@@ -289,20 +287,18 @@ int render_frame(WorldState &w, const CameraModel &cam, size_t width, size_t hei
             HIP_TRY(hipMemcpy(d->cam_nodes, ct.qnodes.data(), ct.qnodes.size() * 4, hipMemcpyHostToDevice));
             HIP_TRY(hipMalloc((void **)&d->cam_tris, ct.tris.size() * 4));
             HIP_TRY(hipMemcpy(d->cam_tris, ct.tris.data(), ct.tris.size() * 4, hipMemcpyHostToDevice));
-            HIP_TRY(hipMalloc((void **)&d->cam_miss, ct.miss.size() * 4));
-            HIP_TRY(hipMemcpy(d->cam_miss, ct.miss.data(), ct.miss.size() * 4, hipMemcpyHostToDevice));
-            d->cam_nnodes = (uint32_t)(ct.qnodes.size() / 4);
+            d->cam_nnodes = (uint32_t)(ct.qnodes.size() / 8);
         }
         d->cam_version = w.ctree_version;
     }
     if (use_tbvh) {
         if (d->cam_nnodes && std::memcmp(w.ctree.origin, &cam.origin, 12) == 0) {
-            p.cam_nodes = d->cam_nodes; p.cam_miss = d->cam_miss; p.cam_tris = d->cam_tris;
+            p.cam_nodes = d->cam_nodes; p.cam_tris = d->cam_tris;
             p.cam_nnodes = d->cam_nnodes;
             for (int k = 0; k < 3; ++k) { p.cq_base[k] = w.ctree.qbox.base[k]; p.cq_step[k] = w.ctree.qbox.step[k]; }
         }
         const TriangleBVH &tb = w.tbvh;
-        p.tbvh_nodes = d->tbvh_nodes; p.tbvh_miss = d->tbvh_miss;
+        p.tbvh_nodes = d->tbvh_nodes;
         p.tbvh_tris = d->tbvh_tris; p.tbvh_loose = d->tbvh_loose;
         p.tnodes = d->tnodes; p.ttris = d->ttris; p.tloose = d->tloose;
         for (int k = 0; k < 3; ++k) {

@@ -37,11 +37,10 @@ struct DeviceState {
     uint32_t nnodes = 0, nbig = 0, nprims = 0;
     uint4 *tbvh_nodes = nullptr;                                // triangle BVH (bvh.h qnodes)
     float4 *tbvh_tris = nullptr;
-    uint32_t *tbvh_miss = nullptr, *tbvh_loose = nullptr;
+    uint32_t *tbvh_loose = nullptr;
     uint32_t tnodes = 0, ttris = 0, tloose = 0;
     uint4 *cam_nodes = nullptr;                                 // camera-origin triangle BVH
     float4 *cam_tris = nullptr;
-    uint32_t *cam_miss = nullptr;
     uint32_t cam_nnodes = 0;
     uint64_t cam_version = 0;                                  // WorldState::ctree_version uploaded
     size_t lds_bytes = 0;                                       // 0: tree not LDS-stageable

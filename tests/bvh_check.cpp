@@ -77,8 +77,9 @@ static void check_tree(const std::vector<float> &nodes, size_t stride, size_t np
 }
 
 static void check_quant(const std::vector<float> &nodes, size_t stride, const std::vector<uint32_t> &q,
-                        const QuantGrid &g, float nb, float ns, const char *what) {
-    const size_t n = nodes.size() / stride, words = stride == 16 ? 8 : 4;
+                        const std::vector<uint32_t> &miss, const QuantGrid &g, float nb, float ns,
+                        const char *what) {
+    const size_t n = nodes.size() / stride, words = 8;
     CHECK(q.size() == n * words, "%s: qnodes size\n", what);
     auto dec = [](uint32_t v, float s, float b) { return std::fmaf((float)v, s, b); };
     for (size_t i = 0; i < n && q.size() == n * words; ++i) {
@@ -98,7 +99,8 @@ static void check_quant(const std::vector<float> &nodes, size_t stride, const st
                 CHECK(dec(m[3 + k], ns, nb) >= f[12 + k], "%s: node %zu nhi %d\n", what, i, k);
             }
         }
-        const uint32_t a = bits(f[3]), b = bits(f[7]), word = w[words == 8 ? 6 : 3];
+        const uint32_t a = bits(f[3]), b = bits(f[7]), word = w[stride == 16 ? 6 : 3];
+        CHECK(w[stride == 16 ? 7 : 4] == miss[i * 8], "%s: link word %zu\n", what, i);
         if (a & kLeafBit)
             CHECK(word == (kLeafBit | ((a & ~kLeafBit) << 3) | b), "%s: leaf word %zu\n", what, i);
         else
@@ -124,12 +126,12 @@ int main(int argc, char **argv) {
     if (!tb.nodes.empty()) {
         check_tree(tb.nodes, 16, tb.tris.size() / 16, leaf, "static");
         check_links(tb.nodes, 16, tb.miss, "static");
-        check_quant(tb.nodes, 16, tb.qnodes, tb.qbox, tb.nbase, tb.nstep, "static");
+        check_quant(tb.nodes, 16, tb.qnodes, tb.miss, tb.qbox, tb.nbase, tb.nstep, "static");
         const float o[3] = {s.camera.origin.x, s.camera.origin.y, s.camera.origin.z};
         cb = build_camera_triangle_bvh(s.triangles, p.tri_hot, tb, o, leaf);
         check_tree(cb.nodes, 8, cb.tris.size() / 16, leaf, "camera");
         check_links(cb.nodes, 8, cb.miss, "camera");
-        check_quant(cb.nodes, 8, cb.qnodes, cb.qbox, 0, 1, "camera");
+        check_quant(cb.nodes, 8, cb.qnodes, cb.miss, cb.qbox, 0, 1, "camera");
         CHECK(cb.tris.size() == tb.tris.size(), "camera tree holds %zu records, static %zu\n",
               cb.tris.size() / 16, tb.tris.size() / 16);
     }
