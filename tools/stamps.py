@@ -21,5 +21,5 @@ for accel in (R.ACCEL_BVH, R.ACCEL_BRUTE):
     c = st["stamp_cycles"]
     tot = sum(c)
     print(cfg, "accel", accel, "trace_ms %.3f" % st["trace_ms"], "shares:",
-          " ".join(f"{n}={x / tot:.3f}" for n, x in zip(["refill", "spheres", "shade", "store"], c)),
+          " ".join(f"{n}={x / tot:.3f}" for n, x in zip(["refill+store", "setup", "walks", "shade"], c)),
           "cycles/ray %.0f" % (tot / st["rays"]))
