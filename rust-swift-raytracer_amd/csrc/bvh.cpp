@@ -485,6 +485,12 @@ CameraTriangleBVH build_camera_triangle_bvh(const std::vector<Triangle> &tris,
     for (uint32_t oct = 0; oct < 8; ++oct) b.links(0, kNodeEnd, oct, out.miss);
     out.tris = triangle_records(prims, tris, tri_hot);
     quantize_boxes(out.nodes, 8, false, out.miss, out.qnodes, out.qbox, nullptr, nullptr);
+    out.rec_box.resize(prims.size() * 6);
+    for (size_t i = 0; i < prims.size(); ++i)
+        for (int k = 0; k < 3; ++k) {
+            out.rec_box[i * 6 + k] = down(prims[i].box.lo[k]);
+            out.rec_box[i * 6 + 3 + k] = up(prims[i].box.hi[k]);
+        }
     return out;
 }
 
@@ -561,6 +567,86 @@ SphereBVH build_sphere_bvh(const std::vector<Sphere> &spheres, uint32_t leaf_siz
         out.prims[i * 4 + 3] = s.radius * s.radius;  // same bits as the brute-force table
         out.prim_id[i] = prims[i].id;
     }
+    return out;
+}
+
+}  // namespace rtamd
+
+namespace rtamd {
+
+PrimaryTriLists build_primary_tri_lists(const CameraTriangleBVH &ct, const CameraModel &cam,
+                                        size_t width, size_t height) {
+    PrimaryTriLists out;
+    const size_t n = ct.rec_box.size() / 6;
+    if (n == 0 || width < 2 || height < 2 || height > (1u << 24) || width > (1u << 24)) return out;
+    const double o[3] = {cam.origin.x, cam.origin.y, cam.origin.z};
+    // ray direction = M (u, v, 1) with M = [h | v | llc - o]  (camera.rs:84-89)
+    double M[3][3];
+    const Vec3 cols[3] = {cam.horizontal, cam.vertical, {cam.lower_left.x - cam.origin.x,
+                                                         cam.lower_left.y - cam.origin.y,
+                                                         cam.lower_left.z - cam.origin.z}};
+    for (int j = 0; j < 3; ++j) { M[0][j] = cols[j].x; M[1][j] = cols[j].y; M[2][j] = cols[j].z; }
+    const double det = M[0][0] * (M[1][1] * M[2][2] - M[1][2] * M[2][1]) -
+                       M[0][1] * (M[1][0] * M[2][2] - M[1][2] * M[2][0]) +
+                       M[0][2] * (M[1][0] * M[2][1] - M[1][1] * M[2][0]);
+    if (!(std::fabs(det) > 0) || !std::isfinite(det)) return out;
+    double Mi[3][3];  // inverse via the adjugate
+    Mi[0][0] = (M[1][1] * M[2][2] - M[1][2] * M[2][1]) / det;
+    Mi[0][1] = (M[0][2] * M[2][1] - M[0][1] * M[2][2]) / det;
+    Mi[0][2] = (M[0][1] * M[1][2] - M[0][2] * M[1][1]) / det;
+    Mi[1][0] = (M[1][2] * M[2][0] - M[1][0] * M[2][2]) / det;
+    Mi[1][1] = (M[0][0] * M[2][2] - M[0][2] * M[2][0]) / det;
+    Mi[1][2] = (M[0][2] * M[1][0] - M[0][0] * M[1][2]) / det;
+    Mi[2][0] = (M[1][0] * M[2][1] - M[1][1] * M[2][0]) / det;
+    Mi[2][1] = (M[0][1] * M[2][0] - M[0][0] * M[2][1]) / det;
+    Mi[2][2] = (M[0][0] * M[1][1] - M[0][1] * M[1][0]) / det;
+    const double wden = (double)(float)(width - 1), hden = (double)(float)(height - 1);
+    const int64_t W = (int64_t)width, H = (int64_t)height;
+    const uint32_t spr = (uint32_t)((width + kTriStripW - 1) / kTriStripW);
+    out.strips_per_row = spr;
+    std::vector<uint32_t> count((size_t)spr * height + 1, 0), always;
+    struct Span { uint32_t rec, s0, s1, r0, r1; };
+    std::vector<Span> spans;
+    spans.reserve(n);
+    for (uint32_t i = 0; i < n; ++i) {
+        const float *b = &ct.rec_box[(size_t)i * 6];
+        double umin = 1e300, umax = -1e300, vmin = 1e300, vmax = -1e300;
+        int front = 0, behind = 0;
+        for (int c = 0; c < 8; ++c) {
+            const double P[3] = {(c & 1 ? b[3] : b[0]) - o[0], (c & 2 ? b[4] : b[1]) - o[1],
+                                 (c & 4 ? b[5] : b[2]) - o[2]};
+            double w[3];
+            for (int r = 0; r < 3; ++r) w[r] = Mi[r][0] * P[0] + Mi[r][1] * P[1] + Mi[r][2] * P[2];
+            const double wn = std::fabs(w[0]) + std::fabs(w[1]) + std::fabs(w[2]);
+            if (w[2] > 1e-6 * wn) {
+                ++front;
+                umin = std::min(umin, w[0] / w[2]); umax = std::max(umax, w[0] / w[2]);
+                vmin = std::min(vmin, w[1] / w[2]); vmax = std::max(vmax, w[1] / w[2]);
+            } else if (w[2] < -1e-6 * wn) {
+                ++behind;
+            }
+        }
+        if (behind == 8) continue;  // no point of positive depth
+        if (front < 8) { always.push_back(i); continue; }
+        // pixel col covers u in [col, col + 1] / wden; one pixel of margin each side
+        const double cl = std::floor(umin * wden) - 2, ch = std::floor(umax * wden) + 1;
+        const double rl = std::floor(vmin * hden) - 2, rh = std::floor(vmax * hden) + 1;
+        if (ch < 0 || cl > (double)(W - 1) || rh < 0 || rl > (double)(H - 1)) continue;
+        const int64_t c0 = std::max<int64_t>(0, (int64_t)cl), c1 = std::min<int64_t>(W - 1, (int64_t)ch);
+        const int64_t r0 = std::max<int64_t>(0, (int64_t)rl), r1 = std::min<int64_t>(H - 1, (int64_t)rh);
+        const Span sp{i, (uint32_t)(c0 / kTriStripW), (uint32_t)(c1 / kTriStripW), (uint32_t)r0, (uint32_t)r1};
+        spans.push_back(sp);
+        for (uint32_t r = sp.r0; r <= sp.r1; ++r)
+            for (uint32_t s = sp.s0; s <= sp.s1; ++s) ++count[(size_t)r * spr + s + 1];
+    }
+    for (size_t k = 1; k < count.size(); ++k) count[k] += count[k - 1];
+    out.offsets = count;
+    out.items.assign(count.back() + always.size(), 0);
+    std::vector<uint32_t> fill(count.begin(), count.end() - 1);
+    for (const Span &sp : spans)
+        for (uint32_t r = sp.r0; r <= sp.r1; ++r)
+            for (uint32_t s = sp.s0; s <= sp.s1; ++s) out.items[fill[(size_t)r * spr + s]++] = sp.rec;
+    std::copy(always.begin(), always.end(), out.items.begin() + count.back());
     return out;
 }
 

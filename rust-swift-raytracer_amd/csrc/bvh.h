@@ -98,9 +98,29 @@ struct CameraTriangleBVH {
     uint32_t depth = 0;
     std::vector<uint32_t> qnodes;   // kernel nodes, 8 u32: box (6 x u16), a, link, 0 0 0
     QuantGrid qbox;
+    std::vector<float> rec_box;     // per record (tris order): padded phantom box lo.xyz, hi.xyz
 };
 CameraTriangleBVH build_camera_triangle_bvh(const std::vector<Triangle> &tris,
                                             const std::vector<float> &tri_hot, const TriangleBVH &tb,
                                             const float origin[3], uint32_t leaf_size);
+
+// Primary-ray triangle lists.  A bounce-0 ray of pixel (col, row) starts at
+// the camera origin o and points into the pixel's footprint, u in
+// [col, col + 1] / (W - 1), v in [row, row + 1] / (H - 1) (common.rs:335-336,
+// camera.rs:84-89).  A camera-tree record can only be accepted by such a ray
+// if its padded phantom box (rec_box) meets that footprint's frustum, so
+// each strip of kTriStripW pixels of one row lists the records whose box
+// projects (through o, onto the image plane) near it, with a one-pixel
+// margin for the rounding of u, v and the direction.  Boxes not entirely in
+// front of the camera go to the `always` list; boxes entirely behind it are
+// dropped (a primary ray only reaches points with positive depth).
+constexpr uint32_t kTriStripW = 8;
+struct PrimaryTriLists {
+    std::vector<uint32_t> offsets;  // strips + 1 (CSR over items); the `always`
+    std::vector<uint32_t> items;    // records follow at [offsets.back(), items.size())
+    uint32_t strips_per_row = 0;
+};
+PrimaryTriLists build_primary_tri_lists(const CameraTriangleBVH &ct, const CameraModel &cam,
+                                        size_t width, size_t height);
 
 }  // namespace rtamd

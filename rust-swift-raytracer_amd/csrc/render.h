@@ -11,6 +11,7 @@ namespace rtamd {
 
 enum : uint32_t { kRngCounter = 1, kRngReplay = 2 };
 enum : uint32_t { kMatDiffuse = 0, kMatMetal = 1, kMatDielectric = 2, kMatEmission = 3 };
+constexpr uint32_t kPrimaryTriStripW = 8;  // bvh.h kTriStripW
 
 // Kernel argument block (lives in the kernarg segment -> SGPRs).
 struct TraceParams {
@@ -68,6 +69,12 @@ struct TraceParams {
     const uint4 *cam_nodes;   // 2 per node: quantised box, a, link
     const float4 *cam_tris;   // 4 per triangle, as tbvh_tris
     uint32_t cam_nnodes;
+    // primary-ray triangle lists (bvh.h PrimaryTriLists, camera-tree record
+    // indices); ptl_off == nullptr: bounce-0 lanes walk the camera tree
+    const uint32_t *ptl_off;  // strips + 1
+    const uint32_t *ptl_items;
+    uint32_t ptl_spr;         // strips per image row
+    uint32_t ptl_always, ptl_end;  // items[ptl_always, ptl_end): tested by every primary ray
 };
 
 hipError_t launch_trace(const TraceParams &p, uint32_t blocks, hipStream_t stream);

@@ -439,6 +439,37 @@ __device__ __forceinline__ void tri_leaf(const TraceParams &p, F3 org, F3 dir, b
         tri_record(recs + 4u * j, org, dir, best_t, tri_t, tri_i, tri_in);
 }
 
+// Job -> (sample, column, row): job = s*npix + local pixel (sample-major);
+// local rows map to image rows through the rank's row blocks (tiles.py);
+// row counts from the bottom as ray_trace does (common.rs:327-331).
+__device__ __forceinline__ void job_pixel(const TraceParams &p, uint32_t job, uint32_t &s,
+                                          uint32_t &col, uint32_t &row) {
+    s = fdiv(job, p.div_npix);
+    const uint32_t lp = job - s * p.npix;
+    const uint32_t q = fdiv(lp, p.div_width);
+    col = lp - q * p.width;
+    const uint32_t lr = p.slab_row0 + q;
+    const uint32_t blk = fdiv(lr, p.div_rowblock);
+    const uint32_t ir = (blk * p.nranks + p.rank) * p.row_block + (lr - blk * p.row_block);
+    row = p.height - 1u - ir;
+}
+
+// Primary ray against its pixel strip's candidate records (bvh.h
+// PrimaryTriLists) plus the `always` records, in any order (tri_merge).
+__device__ __forceinline__ void tri_primary_list(const TraceParams &p, uint32_t job, F3 org, F3 dir,
+                                                 float best_t, float &tri_t, int &tri_i,
+                                                 uint32_t &tri_in, uint32_t &tri_done) {
+    uint32_t s, col, row;
+    job_pixel(p, job, s, col, row);
+    const uint32_t strip = row * p.ptl_spr + col / kPrimaryTriStripW;
+    const uint32_t b = p.ptl_off[strip], e = p.ptl_off[strip + 1];
+    tri_done += (e - b) + (p.ptl_end - p.ptl_always);
+    for (uint32_t j = b; j < e; ++j)
+        tri_record(p.cam_tris + 4u * p.ptl_items[j], org, dir, best_t, tri_t, tri_i, tri_in);
+    for (uint32_t j = p.ptl_always; j < p.ptl_end; ++j)
+        tri_record(p.cam_tris + 4u * p.ptl_items[j], org, dir, best_t, tri_t, tri_i, tri_in);
+}
+
 // ------------------------------------------------------------ trace kernel
 // kBvh: sphere search through the exact BVH (else brute force).  kLds: the
 // tree is copied into the workgroup's LDS once (persistent grid), so every
@@ -570,15 +601,9 @@ __attribute__((amdgpu_waves_per_eu(RT_WAVES_PER_EU, 8))) void trace_kernel(Trace
                 // colours to consecutive slab slots, and the resolve reads
                 // coalesce.  Seeds and replay states use the reference's job
                 // index below, so the enumeration order changes no bits.
-                const uint32_t s = fdiv(job, p.div_npix);
-                const uint32_t lp = job - s * p.npix;
+                uint32_t s, col, row;
+                job_pixel(p, job, s, col, row);
                 slot = job;
-                const uint32_t q = fdiv(lp, p.div_width);
-                const uint32_t col = lp - q * p.width;
-                const uint32_t lr = p.slab_row0 + q;
-                const uint32_t blk = fdiv(lr, p.div_rowblock);
-                const uint32_t ir = (blk * p.nranks + p.rank) * p.row_block + (lr - blk * p.row_block);
-                const uint32_t row = p.height - 1u - ir;
                 const uint64_t gjob = ((uint64_t)row * p.width + col) * p.spp + s;
                 rng = (p.mode == kRngReplay) ? p.replay[gjob] : counter_seed(p.seed, gjob);
                 // common.rs:335-337: u drawn before v; camera.rs:84-89
@@ -662,10 +687,14 @@ __attribute__((amdgpu_waves_per_eu(RT_WAVES_PER_EU, 8))) void trace_kernel(Trace
             tri_i = -1;
             phase = kShade;
             if (p.tnodes != 0) {
-                if (tri_begin(p, org, dir, best_t, bounce == 0 && p.cam_nnodes != 0, e, tri_t, tri_i,
-                              tri_in, tri_done)) {
-                    node = 0;
-                    phase = kTri;
+                const bool cam = bounce == 0 && p.cam_nnodes != 0;
+                if (tri_begin(p, org, dir, best_t, cam, e, tri_t, tri_i, tri_in, tri_done)) {
+                    if (cam && p.ptl_off != nullptr) {
+                        tri_primary_list(p, slot, org, dir, best_t, tri_t, tri_i, tri_in, tri_done);
+                    } else {
+                        node = 0;
+                        phase = kTri;
+                    }
                 }
             } else {
                 triangles_brute(p, org, dir, best_t, tri_t, tri_i, tri_in);

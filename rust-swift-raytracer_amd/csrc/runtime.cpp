@@ -46,7 +46,7 @@ DeviceState::~DeviceState() {
     void *bufs[] = {sph_hot, sph_cold, tri_hot, tri_geo, mats, samples, out, replay, counter, stats,
                     bvh_nodes, bvh_prims, big_hot, bvh_miss, bvh_prim_id, big_id, bvh_miss16,
                     sph_shade, sph_kind, tbvh_nodes, tbvh_tris, tbvh_loose,
-                    cam_nodes, cam_tris};
+                    cam_nodes, cam_tris, ptl_off, ptl_items};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
     for (hipEvent_t e : ev)
@@ -69,6 +69,7 @@ size_t tile_row(size_t k, uint32_t row_block, uint32_t rank, uint32_t nranks) {
     return ((k / B) * nranks + rank) * B + k % B;
 }
 
+static_assert(kPrimaryTriStripW == kTriStripW, "render.h and bvh.h strip widths");
 static constexpr uint64_t kMaxParts = 1024;  // job-queue partitions (render.hip)
 
 static int device_for(WorldState &w, int want, DeviceState *&out) {
@@ -187,6 +188,21 @@ void prepare_camera(WorldState &w, const CameraModel &cam) {
     ++w.ctree_version;
 }
 
+// Primary-ray triangle lists for this camera and frame size (bvh.h); rebuilt
+// when either (or the camera tree) changes: ~22 ms at C5 on one host core.
+static void prepare_primary_tri_lists(WorldState &w, const CameraModel &cam, size_t width,
+                                      size_t height) {
+    if (w.ptl_version && w.ptl_w == width && w.ptl_h == height && w.ptl_ctree == w.ctree_version &&
+        std::memcmp(&w.ptl_cam, &cam, sizeof(cam)) == 0)
+        return;
+    w.ptl = build_primary_tri_lists(w.ctree, cam, width, height);
+    w.ptl_cam = cam;
+    w.ptl_w = width;
+    w.ptl_h = height;
+    w.ptl_ctree = w.ctree_version;
+    ++w.ptl_version;
+}
+
 template <typename T>
 static hipError_t grow(T *&buf, size_t &cap, size_t n) {
     if (n <= cap) return hipSuccess;
@@ -295,6 +311,32 @@ int render_frame(WorldState &w, const CameraModel &cam, size_t width, size_t hei
         if (d->cam_nnodes && std::memcmp(w.ctree.origin, &cam.origin, 12) == 0) {
             p.cam_nodes = d->cam_nodes; p.cam_tris = d->cam_tris;
             p.cam_nnodes = d->cam_nnodes;
+            if (width >= 2 && height >= 2 && env_u64("RT_AMD_PRIMARY_LISTS", 1) != 0) {
+                prepare_primary_tri_lists(w, cam, width, height);
+                if (d->ptl_version != w.ptl_version) {
+                    for (void *b : {(void *)d->ptl_off, (void *)d->ptl_items})
+                        if (b) HIP_TRY(hipFree(b));
+                    d->ptl_off = d->ptl_items = nullptr;
+                    const PrimaryTriLists &pl = w.ptl;
+                    if (!pl.offsets.empty()) {
+                        HIP_TRY(hipMalloc((void **)&d->ptl_off, pl.offsets.size() * 4));
+                        HIP_TRY(hipMemcpy(d->ptl_off, pl.offsets.data(), pl.offsets.size() * 4,
+                                          hipMemcpyHostToDevice));
+                        HIP_TRY(hipMalloc((void **)&d->ptl_items, std::max<size_t>(pl.items.size(), 1) * 4));
+                        if (!pl.items.empty())
+                            HIP_TRY(hipMemcpy(d->ptl_items, pl.items.data(), pl.items.size() * 4,
+                                              hipMemcpyHostToDevice));
+                    }
+                    d->ptl_version = w.ptl_version;
+                }
+                if (d->ptl_off) {
+                    p.ptl_off = d->ptl_off;
+                    p.ptl_items = d->ptl_items;
+                    p.ptl_spr = w.ptl.strips_per_row;
+                    p.ptl_always = w.ptl.offsets.back();
+                    p.ptl_end = (uint32_t)w.ptl.items.size();
+                }
+            }
             for (int k = 0; k < 3; ++k) { p.cq_base[k] = w.ctree.qbox.base[k]; p.cq_step[k] = w.ctree.qbox.step[k]; }
         }
         const TriangleBVH &tb = w.tbvh;

@@ -43,6 +43,8 @@ struct DeviceState {
     float4 *cam_tris = nullptr;
     uint32_t cam_nnodes = 0;
     uint64_t cam_version = 0;                                  // WorldState::ctree_version uploaded
+    uint32_t *ptl_off = nullptr, *ptl_items = nullptr;         // primary-ray triangle lists
+    uint64_t ptl_version = 0;
     size_t lds_bytes = 0;                                       // 0: tree not LDS-stageable
     float4 *samples = nullptr;       size_t samples_cap = 0;   // per-sample colour slab
     uint32_t *out = nullptr;         size_t out_cap = 0;       // RGBA8 tile (host path)
@@ -63,6 +65,10 @@ struct WorldState {
     TriangleBVH tbvh;
     CameraTriangleBVH ctree;      // for the camera origin of ctree_version
     uint64_t ctree_version = 0;   // 0: none built
+    PrimaryTriLists ptl;          // for ptl_cam at ptl_w x ptl_h (and ctree_version)
+    CameraModel ptl_cam{};
+    size_t ptl_w = 0, ptl_h = 0;
+    uint64_t ptl_ctree = 0, ptl_version = 0;
     std::map<int, std::unique_ptr<DeviceState>> devices;
 };
 

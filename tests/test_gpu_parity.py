@@ -223,7 +223,7 @@ def test_scheduling_knobs_do_not_change_samples(monkeypatch, scene):
                 dict(RT_AMD_STEP="1", RT_AMD_STEPS="5"), dict(RT_AMD_STEP="0"),
                 dict(RT_AMD_REFILL="17"), dict(RT_AMD_LDS="0"),
                 dict(RT_AMD_LDS="0", RT_AMD_STEP="1", RT_AMD_STEPS="3"),
-                dict(RT_AMD_LINEAR_E="1")]:
+                dict(RT_AMD_LINEAR_E="1"), dict(RT_AMD_PRIMARY_LISTS="0")]:
         for k, v in env.items():
             monkeypatch.setenv(k, v)
         out, _ = world.render(w, h, spp, 8)
@@ -379,3 +379,23 @@ def test_triangle_camera_tree_follows_camera_moves():
         assert sb["tri_bvh"] == 1
         assert_bits_equal(b, a, f"frame after move {mv}")
         assert_bits_equal(smb[:, :3], sma[:, :3], f"samples after move {mv}")
+
+
+def test_primary_triangle_lists_follow_camera_and_size():
+    """Bounce-0 rays test per-strip candidate lists built for the camera and
+    the frame size: after every move and at every size each sample equals
+    brute force (includes a camera inside the soup and one looking at the
+    soup from behind)."""
+    src = _triangle_scene(51, 600, size=0.8, spheres=30, grid=8)
+    world = R.World(src)
+    for mv, (w, h) in [((0.0, 0.0, 0.0), (128, 72)), ((0.0, 0.0, 0.0), (97, 61)),
+                       ((0.3, -0.2, -5.0), (120, 80)), ((0.0, 1.5, -9.0), (64, 150)),
+                       ((-2.0, 0.0, 12.0), (80, 45))]:
+        world.move_camera(*mv)
+        a, _ = world.render(w, h, 4, 8, accel=R.ACCEL_BRUTE)
+        sa = world.read_samples(w * h * 4)
+        b, sb = world.render(w, h, 4, 8, accel=R.ACCEL_BVH)
+        smb = world.read_samples(w * h * 4)
+        assert sb["tri_bvh"] == 1
+        assert_bits_equal(b, a, f"frame {mv} {w}x{h}")
+        assert_bits_equal(smb[:, :3], sa[:, :3], f"samples {mv} {w}x{h}")
