@@ -562,6 +562,175 @@ __attribute__((amdgpu_waves_per_eu(RT_WAVES_PER_EU, 8))) void trace_kernel(Trace
     uint32_t prefetch = 0;          // lane 0: counter value of the next chunk, fetched early
     bool prefetch_pending = false;  // wave-uniform
     for (;;) {
+        // Directions that need NVec3::new (maths.rs:111-118) this iteration: the
+        // scattered rays' and the new primary rays' share one normalisation.
+        F3 vdir = dir;
+        bool renorm = false;
+        if (active) {
+            // ---- ray_color's bounce loop (common.rs:267-282) as a lane state
+            // machine: setup -> sphere walk -> triangle walk -> shade.  The walks
+            // advance at most p.steps nodes per loop iteration, so lanes whose
+            // search ends early are shaded and refilled while the others walk on.
+            bool done = false;
+            float out_r = 0.0f, out_g = 0.0f, out_b = 0.0f;
+            if (phase == kSetup) {
+                if ((int32_t)bounce >= p.depth) {
+                    done = true;  // depth exhausted -> (0, 0, 0) (common.rs:284)
+                } else {
+                    ++rays;
+                    // slab-test reciprocals only (not reference arithmetic): v_rcp_f32's
+                    // 1-ulp error moves a slab face by <= 4u|b - lo|, inside e_abs and
+                    // rho; +-0 -> +-inf as with a divide
+                    inv = f3(__builtin_amdgcn_rcpf(dir.x), __builtin_amdgcn_rcpf(dir.y),
+                             __builtin_amdgcn_rcpf(dir.z));
+                    oct = (inv.x < 0.0f ? 1u : 0u) | (inv.y < 0.0f ? 2u : 0u) | (inv.z < 0.0f ? 4u : 0u);
+                    // World::hit, spheres in order with shrinking t_max (common.rs:241-247)
+                    best_t = __builtin_inff();
+                    best_i = -1;
+                    if (kBvh) {
+                        spheres_big(p, org, dir, best_t, best_i);
+                        node = 0;
+                        // (RT_AMD_ABLATE=1: timing-only diagnostic, results are wrong)
+                        phase = (p.ablate & 1u) ? kTriInit : kSph;
+                    } else {
+                        spheres_brute(p, org, dir, best_t, best_i);
+                        phase = kTriInit;
+                    }
+                }
+            }
+            RT_STAMP(1);
+            // kStep: at most p.steps node visits per lane per iteration
+            uint32_t budget = p.steps;
+            if (kBvh && phase == kSph) {
+                constexpr uint32_t kEnd = kLds ? 0xFFFFu : kNodeEndDev;
+                const SphBound bnd = sph_bound(p, org);
+                const float e = sph_inflation(p, bnd, best_t);
+                F3 lo = f3(org.x + e, org.y + e, org.z + e), hi = f3(org.x - e, org.y - e, org.z - e);
+                do {
+                    uint32_t leaf = 0;
+                    sphere_node<kLds>(view, inv, oct, best_t, lo, hi, node, leaf, node_tests);
+                    if (leaf != 0)
+                        sphere_leaf(p, view, org, dir, leaf, best_t, best_i, bnd, lo, hi, sph_tests);
+                } while (node != kEnd && (!kStep || --budget != 0));
+                if (node == kEnd) phase = kTriInit;
+            }
+            if (phase == kTriInit) {
+                // Mesh::hit with t_max = best_t, own closest from +inf (common.rs:178-223)
+                tri_t = __builtin_inff();
+                tri_i = -1;
+                phase = kShade;
+                if (p.tnodes != 0) {
+                    const bool cam = bounce == 0 && p.cam_nnodes != 0;
+                    if (tri_begin(p, org, dir, best_t, cam, e, tri_t, tri_i, tri_in, tri_done)) {
+                        if (cam && p.ptl_off != nullptr) {
+                            tri_primary_list(p, slot, org, dir, best_t, tri_t, tri_i, tri_in, tri_done);
+                        } else {
+                            node = 0;
+                            phase = kTri;
+                        }
+                    }
+                } else {
+                    triangles_brute(p, org, dir, best_t, tri_t, tri_i, tri_in);
+                }
+            }
+            if (phase == kTri) {
+                if (kStep) budget = max(budget, p.steps / 2u);  // a lane that just left the sphere walk
+                const bool cam = bounce == 0 && p.cam_nnodes != 0;
+                const F3 dlt = f3(org.x - p.tbvh_oc[0], org.y - p.tbvh_oc[1], org.z - p.tbvh_oc[2]);
+                do {
+                    uint32_t leaf = 0;
+                    tri_node(p, org, inv, dlt, cam, e, fminf(best_t, tri_t), node, leaf, tnode_tests);
+                    if (leaf != 0) tri_leaf(p, org, dir, cam, leaf, best_t, tri_t, tri_i, tri_in, tri_done);
+                } while (node != kNodeEndDev && (!kStep || --budget != 0));
+                if (node == kNodeEndDev) phase = kShade;
+            }
+            RT_STAMP(2);
+            if (phase == kShade) {
+                phase = kSetup;
+                if (tri_i < 0 && best_i < 0) {
+                    // background (common.rs:276-281): re-normalise, lerp to sky blue
+                    const float t = 0.5f * (unit(dir).y + 1.0f);
+                    const float w = 1.0f - t;
+                    out_r = thr_r * (1.0f * w + 0.5f * t);
+                    out_g = thr_g * (1.0f * w + 0.7f * t);
+                    out_b = thr_b * (1.0f * w + 1.0f * t);
+                    done = true;
+                } else {
+                    F3 pos, nrm;
+                    uint32_t kind;
+                    float cr, cg, cb, param;
+                    if (tri_i >= 0) {  // a triangle wins a tie against a sphere
+                        pos = org + scale(dir, tri_t);
+                        const float4 *g = p.tri_geo + 4u * (uint32_t)tri_i;
+                        const float4 A = g[0], Nn = g[3];
+                        nrm = f3(Nn.x, Nn.y, Nn.z);
+                        const float *m = p.mats + 8u * __float_as_uint(A.w);
+                        kind = __float_as_uint(m[0]);
+                        cr = m[1]; cg = m[2]; cb = m[3]; param = m[4];
+                    } else {
+                        // one round trip: centre/radius, colour/param and kind together
+                        const float4 S = view.shade[2 * best_i];
+                        const float4 M = view.shade[2 * best_i + 1];
+                        kind = view.kinds[best_i];
+                        pos = org + scale(dir, best_t);
+                        nrm = unit(divide(pos - f3(S.x, S.y, S.z), S.w));  // common.rs:95
+                        cr = M.x; cg = M.y; cb = M.z; param = M.w;
+                    }
+                    // Each scatter builds an un-normalised direction `v`; the draws
+                    // of diffuse and metal (random_unit_sphere, common.rs:32-38) and
+                    // the final normalisation are shared code so divergent lanes do
+                    // not execute three copies of the divide/sqrt sequences.
+                    bool next = true, keep_normal = false;
+                    F3 v = nrm;
+                    if (kind == kMatDiffuse || kind == kMatMetal) {
+                        const F3 ru = draw_unit(rng);
+                        if (kind == kMatDiffuse) {  // materials.rs:42-52
+                            v = nrm + ru;
+                            const float eps = 1e-8f;
+                            keep_normal = fabsf(v.x) < eps && fabsf(v.y) < eps && fabsf(v.z) < eps;
+                        } else {  // materials.rs:54-63 (reflect, maths.rs:26-28)
+                            const F3 refl = dir - scale(nrm, 2.0f * dot(dir, nrm));
+                            v = refl + scale(ru, param);
+                            next = dot(v, nrm) >= 0.0f;
+                        }
+                    } else if (kind == kMatDielectric) {  // materials.rs:65-97
+                        F3 n2 = nrm;
+                        float eta = param;
+                        if (dot(dir, nrm) >= 0.0f) { n2 = -nrm; eta = 1.0f / param; }
+                        const float cos_t = dot(-dir, n2);  // maths.rs:31-36
+                        const F3 perp = scale(dir + scale(n2, cos_t), eta);
+                        const F3 par = scale(n2, -__builtin_sqrtf(fabsf(1.0f - dot(perp, perp))));
+                        v = perp + par;
+                        cr = cg = cb = 1.0f;
+                    } else {  // Emission (materials.rs:100-102)
+                        next = false;
+                    }
+                    if (next) {
+                        thr_r = thr_r * cr;
+                        thr_g = thr_g * cg;
+                        thr_b = thr_b * cb;
+                        org = pos;
+                        if (keep_normal) {
+                            dir = nrm;
+                        } else {
+                            vdir = v;  // normalised below, with the new rays' directions
+                            renorm = true;
+                        }
+                        ++bounce;
+                    } else {  // common.rs:273-274: final * colour
+                        out_r = thr_r * cr;
+                        out_g = thr_g * cg;
+                        out_b = thr_b * cb;
+                        done = true;
+                    }
+                }
+            }
+            RT_STAMP(3);
+            if (done) {
+                p.samples[slot] = make_float4(out_r, out_g, out_b, 0.0f);
+                active = false;
+            }
+        }
         // ---- refill lanes whose path ended (active-ray compaction) -------
         const uint64_t dead = __ballot(!active);
         const uint32_t ndead = (uint32_t)__popcll(dead);
@@ -613,7 +782,8 @@ __attribute__((amdgpu_waves_per_eu(RT_WAVES_PER_EU, 8))) void trace_kernel(Trace
                 const F3 vv = f3(p.cam[9], p.cam[10], p.cam[11]);
                 org = f3(p.cam[0], p.cam[1], p.cam[2]);
                 const F3 llc = f3(p.cam[3], p.cam[4], p.cam[5]);
-                dir = unit(((llc + scale(h, u)) + scale(vv, v)) - org);
+                vdir = ((llc + scale(h, u)) + scale(vv, v)) - org;  // normalised below
+                renorm = true;
                 thr_r = thr_g = thr_b = 1.0f;
                 bounce = 0;
                 phase = kSetup;
@@ -627,171 +797,9 @@ __attribute__((amdgpu_waves_per_eu(RT_WAVES_PER_EU, 8))) void trace_kernel(Trace
                 prefetch_pending = true;
             }
         }
+        if (renorm) dir = unit(vdir);
         RT_STAMP(0);
-        if (__ballot(active) == 0) {
-            if (exhausted) break;
-            continue;
-        }
-        if (!active) continue;
-
-        // ---- ray_color's bounce loop (common.rs:267-282) as a lane state
-        // machine: setup -> sphere walk -> triangle walk -> shade.  The walks
-        // advance at most p.steps nodes per loop iteration, so lanes whose
-        // search ends early are shaded and refilled while the others walk on.
-        bool done = false;
-        float out_r = 0.0f, out_g = 0.0f, out_b = 0.0f;
-        if (phase == kSetup) {
-            if ((int32_t)bounce >= p.depth) {
-                done = true;  // depth exhausted -> (0, 0, 0) (common.rs:284)
-            } else {
-                ++rays;
-                // slab-test reciprocals only (not reference arithmetic): v_rcp_f32's
-                // 1-ulp error moves a slab face by <= 4u|b - lo|, inside e_abs and
-                // rho; +-0 -> +-inf as with a divide
-                inv = f3(__builtin_amdgcn_rcpf(dir.x), __builtin_amdgcn_rcpf(dir.y),
-                         __builtin_amdgcn_rcpf(dir.z));
-                oct = (inv.x < 0.0f ? 1u : 0u) | (inv.y < 0.0f ? 2u : 0u) | (inv.z < 0.0f ? 4u : 0u);
-                // World::hit, spheres in order with shrinking t_max (common.rs:241-247)
-                best_t = __builtin_inff();
-                best_i = -1;
-                if (kBvh) {
-                    spheres_big(p, org, dir, best_t, best_i);
-                    node = 0;
-                    // (RT_AMD_ABLATE=1: timing-only diagnostic, results are wrong)
-                    phase = (p.ablate & 1u) ? kTriInit : kSph;
-                } else {
-                    spheres_brute(p, org, dir, best_t, best_i);
-                    phase = kTriInit;
-                }
-            }
-        }
-        RT_STAMP(1);
-        // kStep: at most p.steps node visits per lane per iteration
-        uint32_t budget = p.steps;
-        if (kBvh && phase == kSph) {
-            constexpr uint32_t kEnd = kLds ? 0xFFFFu : kNodeEndDev;
-            const SphBound bnd = sph_bound(p, org);
-            const float e = sph_inflation(p, bnd, best_t);
-            F3 lo = f3(org.x + e, org.y + e, org.z + e), hi = f3(org.x - e, org.y - e, org.z - e);
-            do {
-                uint32_t leaf = 0;
-                sphere_node<kLds>(view, inv, oct, best_t, lo, hi, node, leaf, node_tests);
-                if (leaf != 0)
-                    sphere_leaf(p, view, org, dir, leaf, best_t, best_i, bnd, lo, hi, sph_tests);
-            } while (node != kEnd && (!kStep || --budget != 0));
-            if (node == kEnd) phase = kTriInit;
-        }
-        if (phase == kTriInit) {
-            // Mesh::hit with t_max = best_t, own closest from +inf (common.rs:178-223)
-            tri_t = __builtin_inff();
-            tri_i = -1;
-            phase = kShade;
-            if (p.tnodes != 0) {
-                const bool cam = bounce == 0 && p.cam_nnodes != 0;
-                if (tri_begin(p, org, dir, best_t, cam, e, tri_t, tri_i, tri_in, tri_done)) {
-                    if (cam && p.ptl_off != nullptr) {
-                        tri_primary_list(p, slot, org, dir, best_t, tri_t, tri_i, tri_in, tri_done);
-                    } else {
-                        node = 0;
-                        phase = kTri;
-                    }
-                }
-            } else {
-                triangles_brute(p, org, dir, best_t, tri_t, tri_i, tri_in);
-            }
-        }
-        if (phase == kTri) {
-            if (kStep) budget = max(budget, p.steps / 2u);  // a lane that just left the sphere walk
-            const bool cam = bounce == 0 && p.cam_nnodes != 0;
-            const F3 dlt = f3(org.x - p.tbvh_oc[0], org.y - p.tbvh_oc[1], org.z - p.tbvh_oc[2]);
-            do {
-                uint32_t leaf = 0;
-                tri_node(p, org, inv, dlt, cam, e, fminf(best_t, tri_t), node, leaf, tnode_tests);
-                if (leaf != 0) tri_leaf(p, org, dir, cam, leaf, best_t, tri_t, tri_i, tri_in, tri_done);
-            } while (node != kNodeEndDev && (!kStep || --budget != 0));
-            if (node == kNodeEndDev) phase = kShade;
-        }
-        RT_STAMP(2);
-        if (phase == kShade) {
-            phase = kSetup;
-            if (tri_i < 0 && best_i < 0) {
-                // background (common.rs:276-281): re-normalise, lerp to sky blue
-                const float t = 0.5f * (unit(dir).y + 1.0f);
-                const float w = 1.0f - t;
-                out_r = thr_r * (1.0f * w + 0.5f * t);
-                out_g = thr_g * (1.0f * w + 0.7f * t);
-                out_b = thr_b * (1.0f * w + 1.0f * t);
-                done = true;
-            } else {
-                F3 pos, nrm;
-                uint32_t kind;
-                float cr, cg, cb, param;
-                if (tri_i >= 0) {  // a triangle wins a tie against a sphere
-                    pos = org + scale(dir, tri_t);
-                    const float4 *g = p.tri_geo + 4u * (uint32_t)tri_i;
-                    const float4 A = g[0], Nn = g[3];
-                    nrm = f3(Nn.x, Nn.y, Nn.z);
-                    const float *m = p.mats + 8u * __float_as_uint(A.w);
-                    kind = __float_as_uint(m[0]);
-                    cr = m[1]; cg = m[2]; cb = m[3]; param = m[4];
-                } else {
-                    // one round trip: centre/radius, colour/param and kind together
-                    const float4 S = view.shade[2 * best_i];
-                    const float4 M = view.shade[2 * best_i + 1];
-                    kind = view.kinds[best_i];
-                    pos = org + scale(dir, best_t);
-                    nrm = unit(divide(pos - f3(S.x, S.y, S.z), S.w));  // common.rs:95
-                    cr = M.x; cg = M.y; cb = M.z; param = M.w;
-                }
-                // Each scatter builds an un-normalised direction `v`; the draws
-                // of diffuse and metal (random_unit_sphere, common.rs:32-38) and
-                // the final normalisation are shared code so divergent lanes do
-                // not execute three copies of the divide/sqrt sequences.
-                bool next = true, keep_normal = false;
-                F3 v = nrm;
-                if (kind == kMatDiffuse || kind == kMatMetal) {
-                    const F3 ru = draw_unit(rng);
-                    if (kind == kMatDiffuse) {  // materials.rs:42-52
-                        v = nrm + ru;
-                        const float eps = 1e-8f;
-                        keep_normal = fabsf(v.x) < eps && fabsf(v.y) < eps && fabsf(v.z) < eps;
-                    } else {  // materials.rs:54-63 (reflect, maths.rs:26-28)
-                        const F3 refl = dir - scale(nrm, 2.0f * dot(dir, nrm));
-                        v = refl + scale(ru, param);
-                        next = dot(v, nrm) >= 0.0f;
-                    }
-                } else if (kind == kMatDielectric) {  // materials.rs:65-97
-                    F3 n2 = nrm;
-                    float eta = param;
-                    if (dot(dir, nrm) >= 0.0f) { n2 = -nrm; eta = 1.0f / param; }
-                    const float cos_t = dot(-dir, n2);  // maths.rs:31-36
-                    const F3 perp = scale(dir + scale(n2, cos_t), eta);
-                    const F3 par = scale(n2, -__builtin_sqrtf(fabsf(1.0f - dot(perp, perp))));
-                    v = perp + par;
-                    cr = cg = cb = 1.0f;
-                } else {  // Emission (materials.rs:100-102)
-                    next = false;
-                }
-                if (next) {
-                    thr_r = thr_r * cr;
-                    thr_g = thr_g * cg;
-                    thr_b = thr_b * cb;
-                    org = pos;
-                    dir = keep_normal ? nrm : unit(v);
-                    ++bounce;
-                } else {  // common.rs:273-274: final * colour
-                    out_r = thr_r * cr;
-                    out_g = thr_g * cg;
-                    out_b = thr_b * cb;
-                    done = true;
-                }
-            }
-        }
-        RT_STAMP(3);
-        if (done) {
-            p.samples[slot] = make_float4(out_r, out_g, out_b, 0.0f);
-            active = false;
-        }
+        if (__ballot(active) == 0 && exhausted) break;
     }
 
     // ---- per-wave statistics: one atomic per counter per wave ------------
