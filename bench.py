@@ -130,10 +130,12 @@ def main():
     gathered = torch.empty(nr * max_rows * W * 4, dtype=torch.uint8, device=dev) if nr > 1 else None
     stream = torch.cuda.current_stream(dev)
 
-    def step():
+    def step(with_stats):
+        # timed steps run without counters: the frame is only enqueued (no host
+        # wait), so frames and the RCCL gather pipeline on the stream
         st = world.render_device(W, H, tile.data_ptr(), stream.cuda_stream, spp=spp, depth=depth,
                                  row_block=ROW_BLOCK, rank=rank, nranks=nr, device=local_rank,
-                                 accel=accel)
+                                 accel=accel, stats=with_stats)
         if nr > 1:
             if backend == "nccl":
                 tiles.gather(tile, gathered)  # RCCL all-gather over xGMI
@@ -142,18 +144,24 @@ def main():
         return st
 
     for _ in range(args.warmup):
-        step()
+        step(False)
+    st_warm = step(True)  # counters of one frame (the frame is identical every step)
     torch.cuda.synchronize()
     if nr > 1:
         dist.barrier()
     t0 = time.perf_counter()
-    stats = [step() for _ in range(args.steps)]
+    for _ in range(args.steps):
+        step(False)
     torch.cuda.synchronize()
     if nr > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    # kernel timing for the roofline: HIP events around the trace launches of
+    # frames like the timed ones, on the same stream, right after the timed region
+    stats = [step(True) for _ in range(max(1, min(args.steps, 3)))]
+    assert all(s["rays"] == st_warm["rays"] for s in stats), "frames must be identical"
 
-    rays = sum(s["rays"] for s in stats)
+    rays = st_warm["rays"] * args.steps
     trace_ms = sum(s["trace_ms"] for s in stats) / max(1, sum(s["trace_launches"] for s in stats))
     if nr > 1:
         tdev = dev if backend == "nccl" else torch.device("cpu")

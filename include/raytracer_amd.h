@@ -88,8 +88,11 @@ int rt_render_ex(Rust_CFramebuffer framebuffer, const Rust_WorldHandle *handle,
 
 /* Same, but the tile is written to DEVICE memory `d_rgba` (rt_tile_rows*width
  * RGBA8) on HIP stream `hip_stream` (NULL = the library's stream).  The scene
- * stays resident on the device between calls.  Returns after the frame is
- * complete.  Returns 0 or a negative error. */
+ * stays resident on the device between calls.  With `stats`, returns after the
+ * frame is complete (HIP-event timings and counters filled in); with
+ * stats == NULL the frame is only enqueued on the stream (no host wait), so
+ * consecutive frames and the caller's collectives pipeline.  Returns 0 or a
+ * negative error. */
 int rt_render_device(const Rust_WorldHandle *handle, size_t width, size_t height,
                      const RtRenderOptions *opts, void *d_rgba, void *hip_stream,
                      RtRenderStats *stats);

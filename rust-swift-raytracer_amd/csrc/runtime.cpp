@@ -363,6 +363,7 @@ int render_frame(WorldState &w, const CameraModel &cam, size_t width, size_t hei
     const uint64_t full_blocks = (uint64_t)bpc * (uint64_t)d->num_cus;
     double trace_ms = 0.0, resolve_ms = 0.0;
     uint32_t launches = 0, waves = 0;
+    const bool timed = stats != nullptr;  // HIP-event timing + counters need a host wait
     for (size_t r0 = 0; r0 < T; r0 += rows_per_slab) {
         const size_t rows = std::min(rows_per_slab, T - r0);
         const uint64_t njobs = rows * jobs_per_row;
@@ -370,7 +371,7 @@ int render_frame(WorldState &w, const CameraModel &cam, size_t width, size_t hei
         p.njobs = (uint32_t)njobs;
         p.npix = (uint32_t)(rows * width);
         p.div_npix = make_fastdiv(p.npix);
-        HIP_TRY(hipEventRecord(d->ev[0], s));
+        if (timed) HIP_TRY(hipEventRecord(d->ev[0], s));
         if (njobs) {
             const uint64_t jobs_per_block = waves_per_block * 256;
             uint64_t blocks = std::min<uint64_t>(full_blocks, (njobs + jobs_per_block - 1) / jobs_per_block);
@@ -389,17 +390,21 @@ int render_frame(WorldState &w, const CameraModel &cam, size_t width, size_t hei
             ++launches;
             waves = (uint32_t)nwaves;
         }
-        HIP_TRY(hipEventRecord(d->ev[1], s));
+        if (timed) HIP_TRY(hipEventRecord(d->ev[1], s));
         HIP_TRY(launch_resolve_ex(d->samples, d_out, (uint32_t)(rows * width), spp, inv_spp,
                                   (uint32_t)width, (uint32_t)r0, s));
-        HIP_TRY(hipEventRecord(d->ev[2], s));
-        HIP_TRY(hipEventSynchronize(d->ev[2]));
-        float a = 0, b = 0;
-        HIP_TRY(hipEventElapsedTime(&a, d->ev[0], d->ev[1]));
-        HIP_TRY(hipEventElapsedTime(&b, d->ev[1], d->ev[2]));
-        trace_ms += a;
-        resolve_ms += b;
+        if (timed) {
+            HIP_TRY(hipEventRecord(d->ev[2], s));
+            HIP_TRY(hipEventSynchronize(d->ev[2]));
+            float a = 0, b = 0;
+            HIP_TRY(hipEventElapsedTime(&a, d->ev[0], d->ev[1]));
+            HIP_TRY(hipEventElapsedTime(&b, d->ev[1], d->ev[2]));
+            trace_ms += a;
+            resolve_ms += b;
+        }
     }
+    // without stats the frame stays asynchronous on the stream (no host wait)
+    if (!timed) return 0;
     unsigned long long st[16] = {};
     HIP_TRY(hipMemcpyAsync(st, d->stats, 128, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));

@@ -253,15 +253,17 @@ class World:
 
     def render_device(self, width, height, out_ptr: int, stream_ptr: int = 0, spp=16, depth=8,
                       mode=RNG_COUNTER, seed=DEFAULT_SEED, row_block=1, rank=0, nranks=1,
-                      device=-1, accel=ACCEL_AUTO):
-        """rt_render_device into a device buffer (e.g. a torch uint8 tensor)."""
+                      device=-1, accel=ACCEL_AUTO, stats=True):
+        """rt_render_device into a device buffer (e.g. a torch uint8 tensor).
+        stats=False: no counters and no host wait -- the frame is only enqueued
+        on the stream (returns None)."""
         o, _ = options(spp, depth, mode, seed, None, row_block, rank, nranks, device, accel, self._L)
         st = RenderStats()
         rc = self._L.rt_render_device(self._h, width, height, C.byref(o), C.c_void_p(out_ptr),
-                                    C.c_void_p(stream_ptr or None), C.byref(st))
+                                    C.c_void_p(stream_ptr or None), C.byref(st) if stats else None)
         if rc != 0:
             raise RenderError(f"rt_render_device failed ({rc}): {self._L.rt_last_error().decode()}")
-        return st.as_dict()
+        return st.as_dict() if stats else None
 
 
 def write_ppm(rgba: np.ndarray, path: str):
