@@ -10,13 +10,15 @@
 // (-ffp-contract=off, correctly rounded divide/sqrt), so a sample started
 // from the same xorshift32 state produces the same bits as the reference.
 //
-// Work decomposition: one job = one pixel sample.  Each wave is
-// persistent: its 64 lanes trace one bounce per loop iteration; a lane whose
-// path ends writes the sample colour to a per-sample slab in HBM and takes
-// the next job (ballot + mbcnt prefix, one atomic per chunk per wave on one of
-// 64 partitioned counters), so
-// lanes never idle behind the longest path of their wave.  Spheres are read
-// with wave-uniform scalar loads (SGPR operands, scalar cache), never per lane.
+// Work decomposition: one job = one pixel sample.  Each wave
+// is persistent: its 64 lanes trace one bounce per loop iteration; a lane
+// whose path ends writes the sample colour to a per-sample slab in HBM and
+// takes the next job (ballot + mbcnt prefix, one atomic per chunk per wave on
+// one of 64 partitioned counters), so lanes never idle behind the longest path
+// of their wave.  World::hit goes through exact BVHs (spheres: staged in LDS;
+// triangles: phantom-aware static and camera-origin trees, primary strip
+// lists) whose visiting order provably returns the reference's hit; the
+// brute-force loops keep the reference order (RT_ACCEL_BRUTE, small scenes).
 // The resolve kernel sums each pixel's samples in sample order (the
 // reference's sequential add_with_alpha, common.rs:338-340), applies the
 // gamma/`as u8` epilogue (:344-356) and stores RGBA8 rows top-first (:351).
