@@ -399,3 +399,14 @@ def test_primary_triangle_lists_follow_camera_and_size():
         assert sb["tri_bvh"] == 1
         assert_bits_equal(b, a, f"frame {mv} {w}x{h}")
         assert_bits_equal(smb[:, :3], sa[:, :3], f"samples {mv} {w}x{h}")
+
+
+@pytest.mark.parametrize("w,h,spp,depth", [(1, 5, 2, 8), (5, 1, 2, 8), (6, 4, 0, 8), (7, 3, 3, 0)])
+def test_triangle_bvh_edge_frames(w, h, spp, depth):
+    """Degenerate frames (W or H = 1: NaN rays; spp 0; depth 0) through the
+    triangle trees: equal to the oracle bit for bit."""
+    src = _triangle_scene(61, 300, spheres=20)
+    img, st, _ = O.Scene(src).render(w, h, spp, depth, mode=O.RNG_COUNTER)
+    out, gst = R.World(src).render(w, h, spp, depth)
+    assert_bits_equal(out, img, "edge frame")
+    assert gst["rays"] == st["rays"]
