@@ -20,7 +20,7 @@ struct TraceParams {
     const float4 *tri_hot;    // ntri x (n.x, n.y, n.z, n.v0), n = cross(v1-v0, v2-v0)
     const float4 *tri_geo;    // ntri x 4: (v0, mat) (v1, 0) (v2, 0) (unit normal, 0)
     const float *mats;        // 8 floats per material: kind bits, r, g, b, param
-    float4 *samples;          // slab-local per-sample colour (r, g, b, 0)
+    float *samples;           // slab-local sample colours: R, G, B planes of njobs floats
     uint32_t *job_counter;    // nparts counters, 32 u32 apart; zeroed before every launch
     unsigned long long *stats;// rays, tri in t-range, BVH sphere tests, BVH node tests,
                               // 4 stamp counters, triangle-BVH node tests
@@ -79,7 +79,7 @@ struct TraceParams {
 
 hipError_t launch_trace(const TraceParams &p, uint32_t blocks, hipStream_t stream);
 // inv_spp = 1.0 / (spp as f32) computed from the signed spp (common.rs:345).
-hipError_t launch_resolve_ex(const float4 *samples, uint32_t *out, uint32_t npix, uint32_t spp,
+hipError_t launch_resolve_ex(const float *samples, uint32_t *out, uint32_t npix, uint32_t spp,
                              float inv_spp, uint32_t width, uint32_t slab_row0,
                              hipStream_t stream);
 // variant: 0 brute force, 1 BVH from global memory, 2 BVH staged in LDS;

@@ -729,7 +729,10 @@ __attribute__((amdgpu_waves_per_eu(RT_WAVES_PER_EU, 8))) void trace_kernel(Trace
             }
             RT_STAMP(3);
             if (done) {
-                p.samples[slot] = make_float4(out_r, out_g, out_b, 0.0f);
+                // planar slab (R, G, B planes of njobs floats): 12 B per sample
+                p.samples[slot] = out_r;
+                p.samples[(size_t)p.njobs + slot] = out_g;
+                p.samples[2 * (size_t)p.njobs + slot] = out_b;
                 active = false;
             }
         }
@@ -821,21 +824,23 @@ __attribute__((amdgpu_waves_per_eu(RT_WAVES_PER_EU, 8))) void trace_kernel(Trace
 }
 
 // ------------------------------------------------------------ resolve kernel
-// Sums each pixel's samples in order (common.rs:333-341; slab is sample-major,
-// so consecutive threads read consecutive 16-B words), gamma + `as u8`
-// (:344-356), one RGBA8 word per pixel, coalesced along the row.
-__global__ __launch_bounds__(256) void resolve_kernel(const float4 *__restrict__ samples,
+// Sums each pixel's samples in order (common.rs:333-341; the slab is planar
+// and sample-major, so consecutive threads read consecutive floats of each
+// plane), gamma + `as u8` (:344-356), one RGBA8 word per pixel, coalesced
+// along the row.
+__global__ __launch_bounds__(256) void resolve_kernel(const float *__restrict__ samples,
                                                       uint32_t *__restrict__ out, uint32_t npix,
                                                       uint32_t spp, float inv, uint32_t width,
                                                       uint32_t slab_row0) {
     const uint32_t lp = blockIdx.x * blockDim.x + threadIdx.x;
     if (lp >= npix) return;
     float r = 0.0f, g = 0.0f, b = 0.0f, a = 1.0f;  // Color::new(0,0,0): alpha 1
+    const size_t plane = (size_t)npix * spp;
     for (uint32_t k = 0; k < spp; ++k) {
-        const float4 c = samples[(size_t)k * npix + lp];  // sample-major slab
-        r = r + c.x;
-        g = g + c.y;
-        b = b + c.z;
+        const size_t i = (size_t)k * npix + lp;  // sample-major slab
+        r = r + samples[i];
+        g = g + samples[plane + i];
+        b = b + samples[2 * plane + i];
         a = a + 1.0f;  // every sample's alpha is exactly 1.0
     }
     const uint32_t R = sat_u8(__builtin_sqrtf(r * inv) * 255.999f);
@@ -870,7 +875,7 @@ hipError_t launch_trace(const TraceParams &p, uint32_t blocks, hipStream_t strea
     return hipGetLastError();
 }
 
-hipError_t launch_resolve_ex(const float4 *samples, uint32_t *out, uint32_t npix, uint32_t spp,
+hipError_t launch_resolve_ex(const float *samples, uint32_t *out, uint32_t npix, uint32_t spp,
                              float inv_spp, uint32_t width, uint32_t slab_row0,
                              hipStream_t stream) {
     const uint32_t blocks = (npix + 255u) / 256u;

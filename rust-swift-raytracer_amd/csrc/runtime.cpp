@@ -242,7 +242,7 @@ int render_frame(WorldState &w, const CameraModel &cam, size_t width, size_t hei
     const uint64_t slab_jobs = env_u64("RT_AMD_SLAB_JOBS", 1ull << 30);  // 16 GB of slab at most
     size_t rows_per_slab = jobs_per_row ? (size_t)std::max<uint64_t>(1, slab_jobs / jobs_per_row) : T;
     rows_per_slab = std::min(rows_per_slab, T);
-    if (jobs_per_row) HIP_TRY(grow(d->samples, d->samples_cap, rows_per_slab * jobs_per_row));
+    if (jobs_per_row) HIP_TRY(grow(d->samples, d->samples_cap, 3 * rows_per_slab * jobs_per_row));
 
     if (o.rng_mode == RT_RNG_REPLAY && spp) {
         const size_t n = width * height * (size_t)spp;
@@ -436,8 +436,17 @@ long read_samples(WorldState &w, int device, float *out, size_t n) {
     if (rc) return rc;
     const size_t count = std::min(n / 4, d->last_jobs);
     if (!count) return 0;
-    HIP_TRY(hipStreamSynchronize(d->stream));
-    HIP_TRY(hipMemcpy(out, d->samples, count * sizeof(float4), hipMemcpyDeviceToHost));
+    HIP_TRY(hipDeviceSynchronize());
+    std::vector<float> planes(3 * count);
+    for (int c = 0; c < 3; ++c)
+        HIP_TRY(hipMemcpy(planes.data() + c * count, d->samples + c * d->last_jobs, count * sizeof(float),
+                          hipMemcpyDeviceToHost));
+    for (size_t i = 0; i < count; ++i) {  // (r, g, b, 0) per sample, as documented
+        out[4 * i] = planes[i];
+        out[4 * i + 1] = planes[count + i];
+        out[4 * i + 2] = planes[2 * count + i];
+        out[4 * i + 3] = 0.0f;
+    }
     return (long)(count * 4);
 }
 

@@ -46,7 +46,7 @@ struct DeviceState {
     uint32_t *ptl_off = nullptr, *ptl_items = nullptr;         // primary-ray triangle lists
     uint64_t ptl_version = 0;
     size_t lds_bytes = 0;                                       // 0: tree not LDS-stageable
-    float4 *samples = nullptr;       size_t samples_cap = 0;   // per-sample colour slab
+    float *samples = nullptr;        size_t samples_cap = 0;   // sample slab (3 planes)
     uint32_t *out = nullptr;         size_t out_cap = 0;       // RGBA8 tile (host path)
     uint32_t *replay = nullptr;      size_t replay_cap = 0;
     uint32_t *counter = nullptr;                                // job counter
