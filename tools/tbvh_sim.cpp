@@ -31,6 +31,8 @@ static V cross(V a, V b) { return {a.y * b.z - a.z * b.y, -(a.x * b.z - a.z * b.
 static V unit(V a) { float l = std::sqrt(dot(a, a)); return {a.x / l, a.y / l, a.z / l}; }
 
 struct Count { double nodes = 0, tests = 0, rays = 0; };
+static std::vector<int> g_depth;          // node depth (kernel image), for SIM_LEVELS
+static std::vector<double> g_level_visits;
 
 static bool g_exact = false;  // tree over phantom triangles of one origin (no widening)
 
@@ -50,6 +52,7 @@ static float trace(const TriangleBVH &t, V o, V d, Count &c) {
     uint32_t node = 0;
     while (node != kNodeEnd) {
         c.nodes += 1;
+        if (!g_depth.empty()) g_level_visits[g_depth[node]] += 1;
         const uint32_t *w = &t.qnodes[(size_t)node * 8];
         const uint32_t u[6] = {w[0] & 0xFFFF, w[0] >> 16, w[1] & 0xFFFF, w[1] >> 16, w[2] & 0xFFFF, w[2] >> 16};
         const uint32_t m[6] = {w[3] & 0xFFFF, w[3] >> 16, w[4] & 0xFFFF, w[4] >> 16, w[5] & 0xFFFF, w[5] >> 16};
@@ -109,6 +112,18 @@ int main(int argc, char **argv) {
     TriangleBVH t = build_triangle_bvh(s.triangles, p.tri_hot, lf ? std::atoi(lf) : 4);
     std::printf("tris %zu nodes %zu loose %zu depth %u\n", s.triangles.size(), t.nodes.size() / 16,
                 t.loose.size(), t.depth);
+    if (std::getenv("SIM_LEVELS")) {  // depth of every node (child pair at a & 0x1FFFFFFF)
+        const size_t n = t.qnodes.size() / 8;
+        g_depth.assign(n, 0);
+        g_level_visits.assign(64, 0);
+        for (size_t i = 0; i < n; ++i) {  // parents precede children in the builder layout
+            const uint32_t a = t.qnodes[i * 8 + 6];
+            if (!(a & kLeafBit)) {
+                const uint32_t ch = a & 0x1FFFFFFFu;
+                g_depth[ch] = g_depth[ch + 1] = g_depth[i] + 1;
+            }
+        }
+    }
     const CameraModel &cm = s.camera;
     if (std::getenv("SIM_EXACT")) {  // phantom triangles of the camera origin
         g_exact = true;
@@ -185,4 +200,16 @@ int main(int argc, char **argv) {
     if (sec.rays)
         std::printf("secondary: %.0f rays, %.1f nodes/ray, %.1f tests/ray\n", sec.rays,
                     sec.nodes / sec.rays, sec.tests / sec.rays);
+    if (!g_level_visits.empty()) {  // cumulative share of visits in the top levels
+        double tot = 0, acc = 0;
+        std::vector<size_t> per_level(64, 0);
+        for (int d : g_depth) per_level[d]++;
+        for (double v : g_level_visits) tot += v;
+        size_t nodes_acc = 0;
+        for (int d = 0; d < 64 && per_level[d]; ++d) {
+            acc += g_level_visits[d];
+            nodes_acc += per_level[d];
+            std::printf("levels 0..%d: %zu nodes, %.1f%% of visits\n", d, nodes_acc, 100 * acc / tot);
+        }
+    }
 }
