@@ -83,8 +83,8 @@ hipError_t launch_resolve_ex(const float *samples, uint32_t *out, uint32_t npix,
                              float inv_spp, uint32_t width, uint32_t slab_row0,
                              hipStream_t stream);
 // variant: 0 brute force, 1 BVH from global memory, 2 BVH staged in LDS;
-// step: the sliced-walk kernel (TraceParams::step)
-hipError_t trace_occupancy(int *blocks_per_cu, int variant, size_t lds_bytes, bool step);
+// step: the sliced-walk kernel (TraceParams::step); tri: the scene has triangles
+hipError_t trace_occupancy(int *blocks_per_cu, int variant, size_t lds_bytes, bool step, bool tri);
 size_t trace_lds_bytes(const TraceParams &p);
 
 }  // namespace rtamd

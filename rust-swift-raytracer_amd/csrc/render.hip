@@ -485,7 +485,9 @@ __device__ __forceinline__ void tri_primary_list(const TraceParams &p, uint32_t 
 #ifndef RT_WAVES_PER_EU
 #define RT_WAVES_PER_EU 6
 #endif
-template <bool kBvh, bool kLds, bool kStep>
+// kMesh: the scene has triangles (else the whole Mesh::hit stage compiles
+// away, which keeps the sphere-only kernel's register allocation small).
+template <bool kBvh, bool kLds, bool kStep, bool kMesh>
 __global__ __launch_bounds__(kLds ? 512 : 256)
 __attribute__((amdgpu_waves_per_eu(RT_WAVES_PER_EU, 8))) void trace_kernel(TraceParams p) {
     const uint32_t lane = __lane_id();
@@ -621,7 +623,9 @@ __attribute__((amdgpu_waves_per_eu(RT_WAVES_PER_EU, 8))) void trace_kernel(Trace
                 tri_t = __builtin_inff();
                 tri_i = -1;
                 phase = kShade;
-                if (p.tnodes != 0) {
+                if (!kMesh) {
+                    // no triangles: Mesh::hit finds nothing
+                } else if (p.tnodes != 0) {
                     const bool cam = bounce == 0 && p.cam_nnodes != 0;
                     if (tri_begin(p, org, dir, best_t, cam, e, tri_t, tri_i, tri_in, tri_done)) {
                         if (cam && p.ptl_off != nullptr) {
@@ -635,7 +639,7 @@ __attribute__((amdgpu_waves_per_eu(RT_WAVES_PER_EU, 8))) void trace_kernel(Trace
                     triangles_brute(p, org, dir, best_t, tri_t, tri_i, tri_in);
                 }
             }
-            if (phase == kTri) {
+            if (kMesh && phase == kTri) {
                 if (kStep) budget = max(budget, p.steps / 2u);  // a lane that just left the sphere walk
                 const bool cam = bounce == 0 && p.cam_nnodes != 0;
                 const F3 dlt = f3(org.x - p.tbvh_oc[0], org.y - p.tbvh_oc[1], org.z - p.tbvh_oc[2]);
@@ -858,20 +862,28 @@ size_t trace_lds_bytes(const TraceParams &p) {
     return (size_t)p.nnodes * 48 + (size_t)p.nprims * 20 + (size_t)p.nsph_padded * 36;
 }
 
-template <bool kStep>
+template <bool kStep, bool kMesh>
 static void launch_trace_t(const TraceParams &p, uint32_t blocks, hipStream_t stream) {
     if (p.nnodes && p.use_lds)
-        hipLaunchKernelGGL((trace_kernel<true, true, kStep>), dim3(blocks), dim3(512),
+        hipLaunchKernelGGL((trace_kernel<true, true, kStep, kMesh>), dim3(blocks), dim3(512),
                            trace_lds_bytes(p), stream, p);
     else if (p.nnodes)
-        hipLaunchKernelGGL((trace_kernel<true, false, kStep>), dim3(blocks), dim3(256), 0, stream, p);
+        hipLaunchKernelGGL((trace_kernel<true, false, kStep, kMesh>), dim3(blocks), dim3(256), 0, stream,
+                           p);
     else
-        hipLaunchKernelGGL((trace_kernel<false, false, kStep>), dim3(blocks), dim3(256), 0, stream, p);
+        hipLaunchKernelGGL((trace_kernel<false, false, kStep, kMesh>), dim3(blocks), dim3(256), 0, stream,
+                           p);
 }
 
 hipError_t launch_trace(const TraceParams &p, uint32_t blocks, hipStream_t stream) {
-    if (p.step) launch_trace_t<true>(p, blocks, stream);
-    else launch_trace_t<false>(p, blocks, stream);
+    const bool tri = p.ntri != 0;
+    if (p.step) {
+        if (tri) launch_trace_t<true, true>(p, blocks, stream);
+        else launch_trace_t<true, false>(p, blocks, stream);
+    } else {
+        if (tri) launch_trace_t<false, true>(p, blocks, stream);
+        else launch_trace_t<false, false>(p, blocks, stream);
+    }
     return hipGetLastError();
 }
 
@@ -884,21 +896,24 @@ hipError_t launch_resolve_ex(const float *samples, uint32_t *out, uint32_t npix,
     return hipGetLastError();
 }
 
-template <bool kStep>
+template <bool kStep, bool kMesh>
 static hipError_t trace_occupancy_t(int *blocks_per_cu, int variant, size_t lds_bytes) {
     if (variant == 2)
         return hipOccupancyMaxActiveBlocksPerMultiprocessor(
-            blocks_per_cu, trace_kernel<true, true, kStep>, 512, lds_bytes);
+            blocks_per_cu, trace_kernel<true, true, kStep, kMesh>, 512, lds_bytes);
     if (variant == 1)
         return hipOccupancyMaxActiveBlocksPerMultiprocessor(
-            blocks_per_cu, trace_kernel<true, false, kStep>, 256, 0);
-    return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu,
-                                                        trace_kernel<false, false, kStep>, 256, 0);
+            blocks_per_cu, trace_kernel<true, false, kStep, kMesh>, 256, 0);
+    return hipOccupancyMaxActiveBlocksPerMultiprocessor(
+        blocks_per_cu, trace_kernel<false, false, kStep, kMesh>, 256, 0);
 }
 
-hipError_t trace_occupancy(int *blocks_per_cu, int variant, size_t lds_bytes, bool step) {
-    return step ? trace_occupancy_t<true>(blocks_per_cu, variant, lds_bytes)
-                : trace_occupancy_t<false>(blocks_per_cu, variant, lds_bytes);
+hipError_t trace_occupancy(int *blocks_per_cu, int variant, size_t lds_bytes, bool step, bool tri) {
+    if (step)
+        return tri ? trace_occupancy_t<true, true>(blocks_per_cu, variant, lds_bytes)
+                   : trace_occupancy_t<true, false>(blocks_per_cu, variant, lds_bytes);
+    return tri ? trace_occupancy_t<false, true>(blocks_per_cu, variant, lds_bytes)
+               : trace_occupancy_t<false, false>(blocks_per_cu, variant, lds_bytes);
 }
 
 }  // namespace rtamd

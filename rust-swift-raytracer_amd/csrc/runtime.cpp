@@ -94,9 +94,10 @@ static int device_for(WorldState &w, int want, DeviceState *&out) {
         hipDeviceProp_t prop;
         HIP_TRY(hipGetDeviceProperties(&prop, dev));
         d->num_cus = prop.multiProcessorCount;
+        const bool tri = w.packed.ntri > 0;  // the kTri kernels (render.hip)
         for (int st = 0; st < 2; ++st) {
-            HIP_TRY(trace_occupancy(&d->blocks_per_cu[st], 0, 0, st));
-            HIP_TRY(trace_occupancy(&d->blocks_per_cu_bvh[st], 1, 0, st));
+            HIP_TRY(trace_occupancy(&d->blocks_per_cu[st], 0, 0, st, tri));
+            HIP_TRY(trace_occupancy(&d->blocks_per_cu_bvh[st], 1, 0, st, tri));
         }
         // scene upload (once per device)
         const PackedScene &p = w.packed;
@@ -146,7 +147,7 @@ static int device_for(WorldState &w, int want, DeviceState *&out) {
                 HIP_TRY(hipMalloc((void **)&d->bvh_miss16, m16.size() * 2));
                 HIP_TRY(hipMemcpy(d->bvh_miss16, m16.data(), m16.size() * 2, hipMemcpyHostToDevice));
                 for (int st = 0; st < 2; ++st)
-                    HIP_TRY(trace_occupancy(&d->blocks_per_cu_lds[st], 2, lds, st));
+                    HIP_TRY(trace_occupancy(&d->blocks_per_cu_lds[st], 2, lds, st, tri));
                 if (d->blocks_per_cu_lds[0] > 0 && d->blocks_per_cu_lds[1] > 0) d->lds_bytes = lds;
             }
         }
