@@ -86,5 +86,7 @@ hipError_t launch_resolve_ex(const float *samples, uint32_t *out, uint32_t npix,
 // step: the sliced-walk kernel (TraceParams::step); tri: the scene has triangles
 hipError_t trace_occupancy(int *blocks_per_cu, int variant, size_t lds_bytes, bool step, bool tri);
 size_t trace_lds_bytes(const TraceParams &p);
+// threads per trace workgroup: LDS-tree kernels (sphere-only scenes or not) vs global
+uint32_t trace_block_threads(bool lds, bool mesh);
 
 }  // namespace rtamd

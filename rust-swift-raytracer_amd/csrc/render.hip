@@ -485,10 +485,16 @@ __device__ __forceinline__ void tri_primary_list(const TraceParams &p, uint32_t 
 #ifndef RT_WAVES_PER_EU
 #define RT_WAVES_PER_EU 6
 #endif
+// LDS workgroup of the sphere-only kernel.  Measured on C2 (A/B, one
+// process): 512 -> 6.77 ms, 768 -> 6.73, 896 -> 8.41, 1024 (8 waves/SIMD)
+// -> 7.78; above 6 waves per SIMD the per-wave ray state thrashes the L1.
+#ifndef RT_LDS_BLOCK_SPHERES
+#define RT_LDS_BLOCK_SPHERES 512
+#endif
 // kMesh: the scene has triangles (else the whole Mesh::hit stage compiles
 // away, which keeps the sphere-only kernel's register allocation small).
 template <bool kBvh, bool kLds, bool kStep, bool kMesh>
-__global__ __launch_bounds__(kLds ? 512 : 256)
+__global__ __launch_bounds__(kLds ? (kMesh ? 512 : RT_LDS_BLOCK_SPHERES) : 256)
 __attribute__((amdgpu_waves_per_eu(RT_WAVES_PER_EU, 8))) void trace_kernel(TraceParams p) {
     const uint32_t lane = __lane_id();
     extern __shared__ float4 lds[];
@@ -858,6 +864,10 @@ __global__ __launch_bounds__(256) void resolve_kernel(const float *__restrict__ 
 
 }  // namespace
 
+uint32_t trace_block_threads(bool lds, bool mesh) {
+    return lds ? (mesh ? 512u : (uint32_t)RT_LDS_BLOCK_SPHERES) : 256u;
+}
+
 size_t trace_lds_bytes(const TraceParams &p) {
     return (size_t)p.nnodes * 48 + (size_t)p.nprims * 20 + (size_t)p.nsph_padded * 36;
 }
@@ -865,7 +875,8 @@ size_t trace_lds_bytes(const TraceParams &p) {
 template <bool kStep, bool kMesh>
 static void launch_trace_t(const TraceParams &p, uint32_t blocks, hipStream_t stream) {
     if (p.nnodes && p.use_lds)
-        hipLaunchKernelGGL((trace_kernel<true, true, kStep, kMesh>), dim3(blocks), dim3(512),
+        hipLaunchKernelGGL((trace_kernel<true, true, kStep, kMesh>), dim3(blocks),
+                           dim3(trace_block_threads(true, kMesh)),
                            trace_lds_bytes(p), stream, p);
     else if (p.nnodes)
         hipLaunchKernelGGL((trace_kernel<true, false, kStep, kMesh>), dim3(blocks), dim3(256), 0, stream,
@@ -900,7 +911,8 @@ template <bool kStep, bool kMesh>
 static hipError_t trace_occupancy_t(int *blocks_per_cu, int variant, size_t lds_bytes) {
     if (variant == 2)
         return hipOccupancyMaxActiveBlocksPerMultiprocessor(
-            blocks_per_cu, trace_kernel<true, true, kStep, kMesh>, 512, lds_bytes);
+            blocks_per_cu, trace_kernel<true, true, kStep, kMesh>, trace_block_threads(true, kMesh),
+            lds_bytes);
     if (variant == 1)
         return hipOccupancyMaxActiveBlocksPerMultiprocessor(
             blocks_per_cu, trace_kernel<true, false, kStep, kMesh>, 256, 0);

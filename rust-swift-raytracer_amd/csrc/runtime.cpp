@@ -360,7 +360,7 @@ int render_frame(WorldState &w, const CameraModel &cam, size_t width, size_t hei
     p.step = (uint32_t)env_u64("RT_AMD_STEP", use_tbvh ? 1 : 0) != 0;
     const int sv = p.step ? 1 : 0;
     const int bpc = !use_bvh ? d->blocks_per_cu[sv] : p.use_lds ? d->blocks_per_cu_lds[sv] : d->blocks_per_cu_bvh[sv];
-    const uint64_t waves_per_block = (use_bvh && p.use_lds) ? 8 : 4;
+    const uint64_t waves_per_block = trace_block_threads(use_bvh && p.use_lds, p.ntri != 0) / 64;
     const uint64_t full_blocks = (uint64_t)bpc * (uint64_t)d->num_cus;
     double trace_ms = 0.0, resolve_ms = 0.0;
     uint32_t launches = 0, waves = 0;
