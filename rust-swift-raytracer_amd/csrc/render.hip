@@ -191,6 +191,10 @@ struct BvhView {
 // of K s (K = 3e-3) and Kq s^2 / rmin (Kq = 40.5u), both 2.7x the bound,
 // plus e_abs for the slab arithmetic.  A node is skipped only when the
 // inflated box is certainly missed or certainly starts beyond best_t.
+__device__ __forceinline__ float slab_rcp(float d) {
+    return __builtin_amdgcn_fmed3f(__builtin_amdgcn_rcpf(d), -1e20f, 1e20f);
+}
+
 struct SphBound { float A, e_abs; };  // per-ray inputs of the inflation
 __device__ __forceinline__ SphBound sph_bound(const TraceParams &p, F3 org) {
     const float ax = org.x - p.bvh_c[0], ay = org.y - p.bvh_c[1], az = org.z - p.bvh_c[2];
@@ -219,23 +223,24 @@ __device__ __forceinline__ void spheres_big(const TraceParams &p, F3 org, F3 dir
 // pending -- "while-while" -- measured 6% slower on C2 and 60% on C5.)
 template <bool kLds>
 __device__ __forceinline__ void sphere_node(const BvhView &v, F3 inv, uint32_t oct, float best_t,
-                                            F3 lo, F3 hi, uint32_t &node, uint32_t &leaf,
+                                            F3 nlo, F3 nhi, uint32_t &node, uint32_t &leaf,
                                             uint32_t &node_tests) {
     ++node_tests;
     const float4 B0 = v.nodes[2 * node];
     const float4 B1 = v.nodes[2 * node + 1];
     const uint32_t miss = kLds ? (uint32_t)v.miss16[8 * node + oct] : v.miss32[8 * node + oct];
-    // Each computed slab value is (b - lo)(1+d1) * inv(1+d2)(1+d3): the exact
-    // value for a face moved by <= 3u|b - lo|, which e_abs covers, so
-    // [tn, tf] is the exact interval of a box that still contains every
-    // inflated sphere of the node: plain comparisons are safe.
+    // Slab values b * inv - lo * inv as one fma each, nlo = -(lo * inv) per ray
+    // (sphere_slabs): the result is the exact slab value of a face moved by
+    // <= u|lo| + 3u|b - lo| (rounded lo * inv, rcp, the fma's rounding), which
+    // e_abs = 2e-6 (|o|_1 + M) covers ~8x, so [tn, tf] is the exact interval
+    // of a box that still contains every inflated sphere of the node: plain
+    // comparisons are safe.  inv is finite (ray setup), so no 0 * inf NaN.
     // lo = o + e, hi = o - e:  (bmin - e) - o == bmin - (o + e)
-    const float t0x = (B0.x - lo.x) * inv.x, t1x = (B1.x - hi.x) * inv.x;
-    const float t0y = (B0.y - lo.y) * inv.y, t1y = (B1.y - hi.y) * inv.y;
-    const float t0z = (B0.z - lo.z) * inv.z, t1z = (B1.z - hi.z) * inv.z;
+    const float t0x = __builtin_fmaf(B0.x, inv.x, nlo.x), t1x = __builtin_fmaf(B1.x, inv.x, nhi.x);
+    const float t0y = __builtin_fmaf(B0.y, inv.y, nlo.y), t1y = __builtin_fmaf(B1.y, inv.y, nhi.y);
+    const float t0z = __builtin_fmaf(B0.z, inv.z, nlo.z), t1z = __builtin_fmaf(B1.z, inv.z, nhi.z);
     const float tn = fmaxf(fmaxf(fminf(t0x, t1x), fminf(t0y, t1y)), fminf(t0z, t1z));
     const float tf = fminf(fminf(fmaxf(t0x, t1x), fmaxf(t0y, t1y)), fmaxf(t0z, t1z));
-    // NaN (0 * inf on a degenerate slab) compares false: never a skip
     const bool skip = tn > tf || tf < 0.001f || tn > best_t;
     const uint32_t a = __float_as_uint(B0.w);
     const bool is_leaf = (a & kLeafBitDev) != 0;
@@ -244,21 +249,24 @@ __device__ __forceinline__ void sphere_node(const BvhView &v, F3 inv, uint32_t o
     if (!skip && is_leaf) leaf = ((a & ~kLeafBitDev) << 3) | __float_as_uint(B1.w);
 }
 
+// The walk's per-ray slab offsets for inflation e: nlo = -((o + e) inv),
+// nhi = -((o - e) inv).
+__device__ __forceinline__ void sphere_slabs(F3 org, F3 inv, float e, F3 &nlo, F3 &nhi) {
+    nlo = f3(-((org.x + e) * inv.x), -((org.y + e) * inv.y), -((org.z + e) * inv.z));
+    nhi = f3(-((org.x - e) * inv.x), -((org.y - e) * inv.y), -((org.z - e) * inv.z));
+}
+
 // Tests a pending leaf; on a new best, re-derives the inflated origin box.
 __device__ __forceinline__ void sphere_leaf(const TraceParams &p, const BvhView &v, F3 org, F3 dir,
-                                            uint32_t leaf, float &best_t, int &best_i, SphBound bnd,
-                                            F3 &lo, F3 &hi, uint32_t &sph_tests) {
+                                            F3 inv, uint32_t leaf, float &best_t, int &best_i,
+                                            SphBound bnd, F3 &nlo, F3 &nhi, uint32_t &sph_tests) {
     const uint32_t first = leaf >> 3, end = first + (leaf & 7u);
     bool changed = false;
     for (uint32_t j = first; j < end; ++j) {
         ++sph_tests;
         changed |= sphere_candidate(v.prims[j], org, dir, (int)v.ids[j], best_t, best_i);
     }
-    if (changed) {
-        const float e = sph_inflation(p, bnd, best_t);
-        lo = f3(org.x + e, org.y + e, org.z + e);
-        hi = f3(org.x - e, org.y - e, org.z - e);
-    }
+    if (changed) sphere_slabs(org, inv, sph_inflation(p, bnd, best_t), nlo, nhi);
 }
 
 // ------------------------------------------------------------ triangle stage
@@ -590,9 +598,12 @@ __attribute__((amdgpu_waves_per_eu(RT_WAVES_PER_EU, 8))) void trace_kernel(Trace
                     ++rays;
                     // slab-test reciprocals only (not reference arithmetic): v_rcp_f32's
                     // 1-ulp error moves a slab face by <= 4u|b - lo|, inside e_abs and
-                    // rho; +-0 -> +-inf as with a divide
-                    inv = f3(__builtin_amdgcn_rcpf(dir.x), __builtin_amdgcn_rcpf(dir.y),
-                             __builtin_amdgcn_rcpf(dir.z));
+                    // rho.  Clamped to +-1e20 (+-0 -> +-1e20, sign kept)
+                    // so slab products stay finite: an axis with |d| < 1e-20 gets its
+                    // t values scaled by 1e20|d| < 1, which keeps its interval's sign
+                    // pattern -- the ray lies inside that (inflated) slab for any
+                    // finite hit, and the scaled interval still spans [0, >1e9].
+                    inv = f3(slab_rcp(dir.x), slab_rcp(dir.y), slab_rcp(dir.z));
                     oct = (inv.x < 0.0f ? 1u : 0u) | (inv.y < 0.0f ? 2u : 0u) | (inv.z < 0.0f ? 4u : 0u);
                     // World::hit, spheres in order with shrinking t_max (common.rs:241-247)
                     best_t = __builtin_inff();
@@ -614,13 +625,14 @@ __attribute__((amdgpu_waves_per_eu(RT_WAVES_PER_EU, 8))) void trace_kernel(Trace
             if (kBvh && phase == kSph) {
                 constexpr uint32_t kEnd = kLds ? 0xFFFFu : kNodeEndDev;
                 const SphBound bnd = sph_bound(p, org);
-                const float e = sph_inflation(p, bnd, best_t);
-                F3 lo = f3(org.x + e, org.y + e, org.z + e), hi = f3(org.x - e, org.y - e, org.z - e);
+                F3 nlo, nhi;
+                sphere_slabs(org, inv, sph_inflation(p, bnd, best_t), nlo, nhi);
                 do {
                     uint32_t leaf = 0;
-                    sphere_node<kLds>(view, inv, oct, best_t, lo, hi, node, leaf, node_tests);
+                    sphere_node<kLds>(view, inv, oct, best_t, nlo, nhi, node, leaf, node_tests);
                     if (leaf != 0)
-                        sphere_leaf(p, view, org, dir, leaf, best_t, best_i, bnd, lo, hi, sph_tests);
+                        sphere_leaf(p, view, org, dir, inv, leaf, best_t, best_i, bnd, nlo, nhi,
+                                    sph_tests);
                 } while (node != kEnd && (!kStep || --budget != 0));
                 if (node == kEnd) phase = kTriInit;
             }
