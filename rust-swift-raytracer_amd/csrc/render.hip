@@ -379,7 +379,7 @@ __device__ __forceinline__ bool tri_begin(const TraceParams &p, F3 org, F3 dir, 
 
 // One node of the triangle tree (static or camera-origin); an entered leaf is
 // handed back in `leaf` as (first << 3) | count, like sphere_node.
-__device__ __forceinline__ void tri_node(const TraceParams &p, F3 org, F3 inv, F3 dlt, bool cam,
+__device__ __forceinline__ void tri_node(const TraceParams &p, F3 noi, F3 inv, F3 dlt, bool cam,
                                          float rho, float cap, uint32_t &node,
                                          uint32_t &leaf, uint32_t &node_tests) {
     ++node_tests;
@@ -416,19 +416,21 @@ __device__ __forceinline__ void tri_node(const TraceParams &p, F3 org, F3 inv, F
     const float sl = (fminf(ax, bx) + fminf(ay, by)) + fminf(az, bz);
     const float sh = (fmaxf(ax, bx) + fmaxf(ay, by)) + fmaxf(az, bz);
     // phantom offset 2 s m_k over s in [sl, sh], m_k in [N0.k, N1.k]
-    auto widen = [&](float lo, float hi, float m0, float m1, float o, float iv, float &t0, float &t1) {
+    auto widen = [&](float lo, float hi, float m0, float m1, float no, float iv, float &t0, float &t1) {
         const float a = sl * m0, b = sl * m1, c = sh * m0, d = sh * m1;
         const float omin = fminf(fminf(a, b), fminf(c, d));
         const float omax = fmaxf(fmaxf(a, b), fmaxf(c, d));
         const float l = (lo + 2.0f * omin) - rho;
         const float h = (hi + 2.0f * omax) + rho;
-        t0 = (l - o) * iv;
-        t1 = (h - o) * iv;
+        // l * inv - o * inv (noi = -(o * inv)): the face moves by <= u|o| +
+        // 3u|l - o|, far inside rho
+        t0 = __builtin_fmaf(l, iv, no);
+        t1 = __builtin_fmaf(h, iv, no);
     };
     float t0x, t1x, t0y, t1y, t0z, t1z;
-    widen(B0.x, B1.x, N0.x, N1.x, org.x, inv.x, t0x, t1x);
-    widen(B0.y, B1.y, N0.y, N1.y, org.y, inv.y, t0y, t1y);
-    widen(B0.z, B1.z, N0.z, N1.z, org.z, inv.z, t0z, t1z);
+    widen(B0.x, B1.x, N0.x, N1.x, noi.x, inv.x, t0x, t1x);
+    widen(B0.y, B1.y, N0.y, N1.y, noi.y, inv.y, t0y, t1y);
+    widen(B0.z, B1.z, N0.z, N1.z, noi.z, inv.z, t0z, t1z);
     const float tn = fmaxf(fmaxf(fminf(t0x, t1x), fminf(t0y, t1y)), fminf(t0z, t1z));
     const float tf = fminf(fminf(fmaxf(t0x, t1x), fmaxf(t0y, t1y)), fmaxf(t0z, t1z));
     const bool skip = tn > tf || tf < 0.001f || tn > cap;
@@ -661,9 +663,10 @@ __attribute__((amdgpu_waves_per_eu(RT_WAVES_PER_EU, 8))) void trace_kernel(Trace
                 if (kStep) budget = max(budget, p.steps / 2u);  // a lane that just left the sphere walk
                 const bool cam = bounce == 0 && p.cam_nnodes != 0;
                 const F3 dlt = f3(org.x - p.tbvh_oc[0], org.y - p.tbvh_oc[1], org.z - p.tbvh_oc[2]);
+                const F3 noi = f3(-(org.x * inv.x), -(org.y * inv.y), -(org.z * inv.z));
                 do {
                     uint32_t leaf = 0;
-                    tri_node(p, org, inv, dlt, cam, e, fminf(best_t, tri_t), node, leaf, tnode_tests);
+                    tri_node(p, noi, inv, dlt, cam, e, fminf(best_t, tri_t), node, leaf, tnode_tests);
                     if (leaf != 0) tri_leaf(p, org, dir, cam, leaf, best_t, tri_t, tri_i, tri_in, tri_done);
                 } while (node != kNodeEndDev && (!kStep || --budget != 0));
                 if (node == kNodeEndDev) phase = kShade;
