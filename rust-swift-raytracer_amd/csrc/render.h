@@ -27,6 +27,8 @@ struct TraceParams {
     const uint32_t *replay;   // REPLAY start states (global job index)
     float cam[12];            // origin, lower_left, horizontal, vertical
     float wden, hden;         // (width-1) as f32, (height-1) as f32
+    float wrcp, hrcp;         // RN(1/wden), RN(1/hden) (exactdiv.h) ...
+    uint32_t xdiv_uv;         // ... valid when nonzero (both in the exact-division range)
     uint32_t nsph, nsph_padded, ntri;
     uint32_t width, height, spp;
     int32_t depth;            // max_ray_bounces (may be <= 0: zero colour)

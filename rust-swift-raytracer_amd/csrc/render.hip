@@ -26,6 +26,7 @@
 
 #include <cstdint>
 
+#include "exactdiv.h"
 #include "render.h"
 
 #pragma clang fp contract(off)
@@ -41,15 +42,29 @@ __device__ __forceinline__ F3 operator+(F3 a, F3 b) { return F3{a.x + b.x, a.y +
 __device__ __forceinline__ F3 operator-(F3 a, F3 b) { return F3{a.x - b.x, a.y - b.y, a.z - b.z}; }
 __device__ __forceinline__ F3 operator-(F3 a) { return F3{-a.x, -a.y, -a.z}; }
 __device__ __forceinline__ F3 scale(F3 a, float s) { return F3{a.x * s, a.y * s, a.z * s}; }
-__device__ __forceinline__ F3 divide(F3 a, float s) { return F3{a.x / s, a.y / s, a.z / s}; }
 // (x*x' + y*y') + z*z'  (maths.rs:82)
 __device__ __forceinline__ float dot(F3 a, F3 b) { return (a.x * b.x + a.y * b.y) + a.z * b.z; }
 __device__ __forceinline__ F3 cross(F3 a, F3 b) {  // maths.rs:88-94
     return F3{a.y * b.z - a.z * b.y, -(a.x * b.z - a.z * b.x), a.x * b.y - a.y * b.x};
 }
+// The divisions go through exactdiv.h (one shared correctly rounded
+// reciprocal, three corrected quotients: the same bits as `/`) whenever the
+// operands are in its guarded range; HIP's divide otherwise (never taken by
+// lanes of ordinary scenes, so the branch is skipped wave-wide).
+// RT_NO_XDIV builds the plain-divide variant (A/B only).
+__device__ __forceinline__ F3 divide_by(F3 a, float b) {
+#ifndef RT_NO_XDIV
+    // (bitwise: both guards evaluate without a branch)
+    if (__builtin_expect((unsigned)xdiv_den_ok(b) & (unsigned)xdiv_num3_ok(a.x, a.y, a.z), 1)) {
+        const float y = xdiv_rcp(b);
+        return F3{xdiv(a.x, b, y), xdiv(a.y, b, y), xdiv(a.z, b, y)};
+    }
+#endif
+    return F3{a.x / b, a.y / b, a.z / b};
+}
 __device__ __forceinline__ F3 unit(F3 a) {  // NVec3::new, maths.rs:111-118
-    float len = __builtin_sqrtf((a.x * a.x + a.y * a.y) + a.z * a.z);
-    return F3{a.x / len, a.y / len, a.z / len};
+    const float len = __builtin_sqrtf((a.x * a.x + a.y * a.y) + a.z * a.z);
+    return divide_by(a, len);
 }
 
 // xorshift32 (random.rs:22-30) and `x as f32 / u32::MAX as f32` == x * 2^-32.
@@ -700,7 +715,7 @@ __attribute__((amdgpu_waves_per_eu(RT_WAVES_PER_EU, 8))) void trace_kernel(Trace
                         const float4 M = view.shade[2 * best_i + 1];
                         kind = view.kinds[best_i];
                         pos = org + scale(dir, best_t);
-                        nrm = unit(divide(pos - f3(S.x, S.y, S.z), S.w));  // common.rs:95
+                        nrm = unit(divide_by(pos - f3(S.x, S.y, S.z), S.w));  // common.rs:95
                         cr = M.x; cg = M.y; cb = M.z; param = M.w;
                     }
                     // Each scatter builds an un-normalised direction `v`; the draws
@@ -806,8 +821,17 @@ __attribute__((amdgpu_waves_per_eu(RT_WAVES_PER_EU, 8))) void trace_kernel(Trace
                 const uint64_t gjob = ((uint64_t)row * p.width + col) * p.spp + s;
                 rng = (p.mode == kRngReplay) ? p.replay[gjob] : counter_seed(p.seed, gjob);
                 // common.rs:335-337: u drawn before v; camera.rs:84-89
-                const float u = ((float)col + draw01(rng)) / p.wden;
-                const float v = ((float)row + draw01(rng)) / p.hden;
+                // numerators are in [2^-32, 2^24]: exactdiv.h with the host's
+                // reciprocals whenever the denominators are in range
+                const float un = (float)col + draw01(rng);
+                const float vn = (float)row + draw01(rng);
+#ifndef RT_NO_XDIV
+                const bool xd = p.xdiv_uv != 0;
+#else
+                const bool xd = false;
+#endif
+                const float u = xd ? xdiv(un, p.wden, p.wrcp) : un / p.wden;
+                const float v = xd ? xdiv(vn, p.hden, p.hrcp) : vn / p.hden;
                 const F3 h = f3(p.cam[6], p.cam[7], p.cam[8]);
                 const F3 vv = f3(p.cam[9], p.cam[10], p.cam[11]);
                 org = f3(p.cam[0], p.cam[1], p.cam[2]);

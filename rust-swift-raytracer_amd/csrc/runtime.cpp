@@ -264,6 +264,12 @@ int render_frame(WorldState &w, const CameraModel &cam, size_t width, size_t hei
     for (int i = 0; i < 4; ++i) { p.cam[3 * i] = cv[i].x; p.cam[3 * i + 1] = cv[i].y; p.cam[3 * i + 2] = cv[i].z; }
     p.wden = (float)(uint64_t)(width - 1);   // (width-1) as f32 (common.rs:335)
     p.hden = (float)(uint64_t)(height - 1);  // (height-1) as f32 (common.rs:336)
+    // the camera divisions through exactdiv.h: a denominator in [2^-40, 2^40]
+    // and its correctly rounded reciprocal (IEEE division on the host)
+    auto den_ok = [](float b) { return b >= 0x1p-40f && b <= 0x1p40f; };
+    p.xdiv_uv = den_ok(p.wden) && den_ok(p.hden);
+    p.wrcp = p.xdiv_uv ? 1.0f / p.wden : 0.0f;
+    p.hrcp = p.xdiv_uv ? 1.0f / p.hden : 0.0f;
     p.nsph = d->nsph; p.nsph_padded = d->nsph_padded; p.ntri = d->ntri;
     p.width = (uint32_t)width; p.height = (uint32_t)height; p.spp = spp;
     p.depth = o.max_ray_bounces;
