@@ -20,7 +20,8 @@ struct TraceParams {
     const float4 *tri_hot;    // ntri x (n.x, n.y, n.z, n.v0), n = cross(v1-v0, v2-v0)
     const float4 *tri_geo;    // ntri x 4: (v0, mat) (v1, 0) (v2, 0) (unit normal, 0)
     const float *mats;        // 8 floats per material: kind bits, r, g, b, param
-    float *samples;           // slab-local sample colours: R, G, B planes of njobs floats
+    float *samples;           // slab-local sample colours: R, G, B planes of njobs floats,
+                              // pixel-major (slot = job = local pixel * spp + s)
     uint32_t *job_counter;    // nparts counters, 32 u32 apart; zeroed before every launch
     unsigned long long *stats;// rays, tri in t-range, BVH sphere tests, BVH node tests,
                               // 4 stamp counters, triangle-BVH node tests
@@ -36,7 +37,7 @@ struct TraceParams {
     uint32_t row_block, rank, nranks;
     uint32_t slab_row0;       // first tile row of this launch
     uint32_t njobs;           // samples in this launch
-    uint32_t npix;            // pixels in this launch (slab index = s*npix + pixel)
+    uint32_t npix;            // pixels in this launch
     uint32_t chunk;           // jobs fetched per atomic by one wave
     uint32_t nparts;          // job-queue partitions (kernel header comment)
     // exact-pruning BVH (bvh.h); nnodes == 0 selects the brute-force kernel
@@ -52,7 +53,7 @@ struct TraceParams {
     uint32_t ablate;          // timing-only diagnostics (RT_AMD_ABLATE): 1 = skip the tree walk
     const float4 *sph_shade;  // 2 per sphere: (centre, r) (colour, fuzz|ir)
     const uint32_t *sph_kind; // material kind per sphere
-    FastDiv div_npix, div_width, div_rowblock;  // job -> (sample, pixel) mapping
+    FastDiv div_spp, div_width, div_rowblock;  // job -> (pixel, sample) mapping
     uint32_t refill_min;      // refill dead lanes once at least this many are idle
     uint32_t steps;           // BVH nodes a lane walks per loop iteration (>= 1) ...
     uint32_t step;            // ... when nonzero (else walks run to the end)

@@ -279,6 +279,7 @@ int render_frame(WorldState &w, const CameraModel &cam, size_t width, size_t hei
     p.sph_kind = d->sph_kind;
 
     p.div_width = make_fastdiv((uint32_t)width);
+    p.div_spp = make_fastdiv(spp ? spp : 1);
     p.div_rowblock = make_fastdiv(B);
     p.refill_min = (uint32_t)std::max<uint64_t>(1, env_u64("RT_AMD_REFILL", 1));
     p.steps = (uint32_t)std::max<uint64_t>(1, env_u64("RT_AMD_STEPS", 256));
@@ -377,7 +378,6 @@ int render_frame(WorldState &w, const CameraModel &cam, size_t width, size_t hei
         p.slab_row0 = (uint32_t)r0;
         p.njobs = (uint32_t)njobs;
         p.npix = (uint32_t)(rows * width);
-        p.div_npix = make_fastdiv(p.npix);
         if (timed) HIP_TRY(hipEventRecord(d->ev[0], s));
         if (njobs) {
             const uint64_t jobs_per_block = waves_per_block * 256;
@@ -394,6 +394,7 @@ int render_frame(WorldState &w, const CameraModel &cam, size_t width, size_t hei
             HIP_TRY(hipMemsetAsync(d->counter, 0, parts * 128, s));
             HIP_TRY(launch_trace(p, (uint32_t)blocks, s));
             d->last_jobs = njobs;
+            d->last_spp = spp;
             ++launches;
             waves = (uint32_t)nwaves;
         }
@@ -444,14 +445,18 @@ long read_samples(WorldState &w, int device, float *out, size_t n) {
     const size_t count = std::min(n / 4, d->last_jobs);
     if (!count) return 0;
     HIP_TRY(hipDeviceSynchronize());
-    std::vector<float> planes(3 * count);
+    std::vector<float> planes(3 * d->last_jobs);
     for (int c = 0; c < 3; ++c)
-        HIP_TRY(hipMemcpy(planes.data() + c * count, d->samples + c * d->last_jobs, count * sizeof(float),
-                          hipMemcpyDeviceToHost));
-    for (size_t i = 0; i < count; ++i) {  // (r, g, b, 0) per sample, as documented
-        out[4 * i] = planes[i];
-        out[4 * i + 1] = planes[count + i];
-        out[4 * i + 2] = planes[2 * count + i];
+        HIP_TRY(hipMemcpy(planes.data() + c * d->last_jobs, d->samples + c * d->last_jobs,
+                          d->last_jobs * sizeof(float), hipMemcpyDeviceToHost));
+    // (r, g, b, 0) per sample, as documented: sample-major order (s * npix +
+    // pixel) from the pixel-major slab (pixel * spp + s)
+    const size_t spp = std::max<size_t>(1, d->last_spp), npix = d->last_jobs / spp;
+    for (size_t i = 0; i < count; ++i) {
+        const size_t src = (i % npix) * spp + i / npix;
+        out[4 * i] = planes[src];
+        out[4 * i + 1] = planes[d->last_jobs + src];
+        out[4 * i + 2] = planes[2 * d->last_jobs + src];
         out[4 * i + 3] = 0.0f;
     }
     return (long)(count * 4);

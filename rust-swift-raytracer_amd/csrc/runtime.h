@@ -55,6 +55,7 @@ struct DeviceState {
     int blocks_per_cu[2] = {0, 0}, blocks_per_cu_bvh[2] = {0, 0}, blocks_per_cu_lds[2] = {0, 0};
     int num_cus = 0;
     size_t last_jobs = 0;                                       // jobs of the last launch
+    size_t last_spp = 0;                                        // and its spp
     ~DeviceState();
 };
 
