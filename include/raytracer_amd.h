@@ -37,7 +37,16 @@ typedef struct RtRenderOptions {
   uint32_t nranks;                /* nranks; this call renders rank's rows      */
   int32_t device;                 /* HIP device ordinal, -1 = current device    */
   int32_t accel;                  /* RT_ACCEL_*: how World::hit finds spheres   */
+  uint32_t flags;                 /* RT_FLAG_* (0 = default)                    */
 } RtRenderOptions;
+
+/* Frame resolve.  By default the trace kernel resolves each pixel itself: a
+ * wave keeps its chunks' samples in a small per-wave ring (cache-resident)
+ * and sums a pixel's samples in order once its last sample is done, so only
+ * the RGBA8 frame reaches HBM.  RT_FLAG_KEEP_SAMPLES writes every sample to a
+ * full slab in HBM instead and resolves with a second kernel, which
+ * rt_read_samples can then read.  Both give bit-identical frames. */
+enum { RT_FLAG_KEEP_SAMPLES = 1 };
 
 /* Sphere search.  Both give bit-identical frames:
  *   RT_ACCEL_BRUTE: every sphere in file order (common.rs:241-247).
@@ -66,7 +75,8 @@ typedef struct RtRenderStats {
   uint64_t tri_node_tests;   /* triangle-BVH node tests executed              */
   uint64_t bvh_tri_tests;    /* triangle tests executed (== tri_tests brute)  */
   uint32_t tri_bvh;          /* 1 when the triangle BVH ran                   */
-  uint32_t reserved;
+  uint32_t fused_resolve;    /* 1 when the trace kernel resolved the pixels
+                                (no slab, resolve_ms ~ 0)                    */
 } RtRenderStats;
 
 /* spp 16, depth 8 (lib.rs:51), COUNTER, seed 2547549, one rank, device -1. */
@@ -99,9 +109,10 @@ int rt_render_device(const Rust_WorldHandle *handle, size_t width, size_t height
 
 /* Diagnostics: copies the per-sample colours (r, g, b, 0 as 4 f32) of the
  * LAST trace launch on `device` (-1 = current) to host `out` (n floats max).
- * Slab order is sample-major: slot = s*(rows*width) + k*width + col for
- * sample s of tile row k (rows = tile rows of that launch).  Returns the
- * number of floats copied or a negative error. */
+ * That launch must have been rendered with RT_FLAG_KEEP_SAMPLES.  Output
+ * order is sample-major: slot = s*(rows*width) + k*width + col for sample s
+ * of tile row k (rows = tile rows of that launch).  Returns the number of
+ * floats copied or a negative error. */
 long rt_read_samples(const Rust_WorldHandle *handle, int device, float *out, size_t n);
 
 /* Frees a handle from load_world (the reference never frees, lib.rs:42-45). */

@@ -12,6 +12,7 @@ namespace rtamd {
 enum : uint32_t { kRngCounter = 1, kRngReplay = 2 };
 enum : uint32_t { kMatDiffuse = 0, kMatMetal = 1, kMatDielectric = 2, kMatEmission = 3 };
 constexpr uint32_t kPrimaryTriStripW = 8;  // bvh.h kTriStripW
+constexpr uint32_t kTraceRing = 4;         // chunk slots per wave (fused resolve)
 
 // Kernel argument block (lives in the kernarg segment -> SGPRs).
 struct TraceParams {
@@ -22,6 +23,15 @@ struct TraceParams {
     const float *mats;        // 8 floats per material: kind bits, r, g, b, param
     float *samples;           // slab-local sample colours: R, G, B planes of njobs floats,
                               // pixel-major (slot = job = local pixel * spp + s)
+    // fused resolve (ring != nullptr, else the samples go to the slab above and
+    // resolve_kernel sums them): each wave owns kTraceRing slots of 2^ring_shift
+    // samples per plane (R, G, B), one chunk per slot; when a chunk's last
+    // sample is done the wave sums its pixels in order and stores RGBA8 to out
+    float *ring;
+    uint32_t ring_shift;
+    uint32_t *out;            // tile RGBA8 words (tile row-major)
+    float inv_spp;            // 1.0 / spp as f32 (common.rs:345)
+    uint32_t alpha_u8;        // the alpha byte: every pixel's is the same (resolve_kernel)
     uint32_t *job_counter;    // nparts counters, 32 u32 apart; zeroed before every launch
     unsigned long long *stats;// rays, tri in t-range, BVH sphere tests, BVH node tests,
                               // 4 stamp counters, triangle-BVH node tests

@@ -497,6 +497,50 @@ __device__ __forceinline__ void tri_primary_list(const TraceParams &p, uint32_t 
         tri_record(p.cam_tris + 4u * p.ptl_items[j], org, dir, best_t, tri_t, tri_i, tri_in);
 }
 
+// Fused resolve of one finished chunk (wave-uniform call): jobs [base, base +
+// len) are whole pixels (chunks and partitions are pixel-aligned), their
+// samples sit at ring offset `off` of the wave's ring (planes `plane` floats
+// apart).  A lane per pixel sums the samples in order (common.rs:333-341,
+// the same fold as resolve_kernel), then gamma + `as u8` (:344-356).  The
+// samples were stored by this wave: a workgroup-scope fence orders them
+// (one CU, one L1).
+__device__ __forceinline__ void resolve_chunk(const TraceParams &p, const float *ring, uint32_t plane,
+                                           uint32_t off, uint32_t base, uint32_t len,
+                                           uint32_t lane) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    const uint32_t spp = p.spp;
+    const uint32_t np = fdiv(len, p.div_spp), pix0 = fdiv(base, p.div_spp);
+    for (uint32_t i = lane; i < np; i += kWave) {
+        const float *src = ring + off + i * spp;
+        float r = 0.0f, g = 0.0f, b = 0.0f;
+        if ((spp & 3u) == 0) {
+#pragma unroll 4
+            for (uint32_t k = 0; k < spp; k += 4) {
+                const float4 R = *reinterpret_cast<const float4 *>(src + k);
+                const float4 G = *reinterpret_cast<const float4 *>(src + plane + k);
+                const float4 B = *reinterpret_cast<const float4 *>(src + 2 * plane + k);
+                r = r + R.x; r = r + R.y; r = r + R.z; r = r + R.w;
+                g = g + G.x; g = g + G.y; g = g + G.z; g = g + G.w;
+                b = b + B.x; b = b + B.y; b = b + B.z; b = b + B.w;
+            }
+        } else {
+            for (uint32_t k = 0; k < spp; ++k) {
+                r = r + src[k];
+                g = g + src[plane + k];
+                b = b + src[2 * plane + k];
+            }
+        }
+        const uint32_t R = sat_u8(__builtin_sqrtf(r * p.inv_spp) * 255.999f);
+        const uint32_t G = sat_u8(__builtin_sqrtf(g * p.inv_spp) * 255.999f);
+        const uint32_t B = sat_u8(__builtin_sqrtf(b * p.inv_spp) * 255.999f);
+        const uint32_t lp = pix0 + i;
+        const uint32_t q = fdiv(lp, p.div_width);
+        const uint32_t col = lp - q * p.width;
+        p.out[(size_t)(p.slab_row0 + q) * p.width + col] = R | (G << 8) | (B << 16) | (p.alpha_u8 << 24);
+    }
+}
+
 // ------------------------------------------------------------ trace kernel
 // kBvh: sphere search through the exact BVH (else brute force).  kLds: the
 // tree is copied into the workgroup's LDS once (persistent grid), so every
@@ -554,7 +598,7 @@ __attribute__((amdgpu_waves_per_eu(RT_WAVES_PER_EU, 8))) void trace_kernel(Trace
 
     F3 org = f3(0, 0, 0), dir = f3(0, 0, 0), inv = f3(0, 0, 0);
     float thr_r = 1.0f, thr_g = 1.0f, thr_b = 1.0f;  // ray_color's final_color
-    uint32_t rng = 0, slot = 0, bounce = 0;
+    uint32_t rng = 0, slot = ~0u, bounce = 0;  // slot ~0: no finished sample to count
     // lane state between loop iterations (see the bounce loop below)
     enum : uint32_t { kSetup = 0, kSph = 1, kTriInit = 2, kTri = 3, kShade = 4 };
     uint32_t phase = kSetup, node = 0, oct = 0;
@@ -566,6 +610,30 @@ __attribute__((amdgpu_waves_per_eu(RT_WAVES_PER_EU, 8))) void trace_kernel(Trace
 
     uint32_t pool_next = 0, pool_end = 0;  // wave-uniform job pool
     bool exhausted = false;
+
+    // Where a finished sample goes: the slab (slot = job) or, with the fused
+    // resolve, the wave's ring (slot = ring offset = (k << ring_shift) + job -
+    // rbase[k] for the chunk in ring slot k).  All wave-uniform.
+    const bool fused = p.ring != nullptr;
+    const uint32_t wave_id = __builtin_amdgcn_readfirstlane(blockIdx.x * (blockDim.x / kWave) +
+                                                            threadIdx.x / kWave);
+    float *const sbase = fused ? p.ring + (size_t)wave_id * (3u * kTraceRing << p.ring_shift)
+                               : p.samples;
+    const uint32_t pstride = fused ? (kTraceRing << p.ring_shift) : p.njobs;
+    uint32_t rfree = (1u << kTraceRing) - 1u;  // ring slots not holding a chunk
+    uint32_t rbase[kTraceRing], rlen[kTraceRing], rleft[kTraceRing];  // chunk jobs, samples not done
+#pragma unroll
+    for (uint32_t k = 0; k < kTraceRing; ++k) rbase[k] = rlen[k] = rleft[k] = 0;
+    uint32_t cur_off = 0;  // slot - job for the pool's chunk
+    // a lane's job from its slot (tri_primary_list needs the pixel)
+    auto lane_job = [&](uint32_t sl) -> uint32_t {
+        if (!fused) return sl;
+        const uint32_t k = sl >> p.ring_shift;
+        uint32_t b = rbase[0];
+#pragma unroll
+        for (uint32_t i = 1; i < kTraceRing; ++i) b = k == i ? rbase[i] : b;
+        return b + (sl & ((1u << p.ring_shift) - 1u));
+    };
 
 #ifdef RT_STAMPS
     // diagnostic build only: wave cycles per loop segment (s_memtime deltas)
@@ -590,8 +658,9 @@ __attribute__((amdgpu_waves_per_eu(RT_WAVES_PER_EU, 8))) void trace_kernel(Trace
     // its home partition and moves on when that one is drained.
     uint32_t part = (blockIdx.x * (blockDim.x / kWave) + threadIdx.x / kWave) % p.nparts;
     uint32_t tries = 0;  // partitions found drained (wave-uniform)
+    // (pixel-aligned, so every chunk holds whole pixels: the fused resolve)
     auto part_begin = [&](uint32_t k) -> uint32_t {
-        return (uint32_t)(((uint64_t)k * p.njobs) / p.nparts);
+        return (uint32_t)(((uint64_t)k * p.npix) / p.nparts) * p.spp;
     };
     uint32_t pbegin = part_begin(part), pend = part_begin(part + 1);
     uint32_t prefetch = 0;          // lane 0: counter value of the next chunk, fetched early
@@ -601,12 +670,12 @@ __attribute__((amdgpu_waves_per_eu(RT_WAVES_PER_EU, 8))) void trace_kernel(Trace
         // scattered rays' and the new primary rays' share one normalisation.
         F3 vdir = dir;
         bool renorm = false;
+        bool done = false;
         if (active) {
             // ---- ray_color's bounce loop (common.rs:267-282) as a lane state
             // machine: setup -> sphere walk -> triangle walk -> shade.  The walks
             // advance at most p.steps nodes per loop iteration, so lanes whose
             // search ends early are shaded and refilled while the others walk on.
-            bool done = false;
             float out_r = 0.0f, out_g = 0.0f, out_b = 0.0f;
             if (phase == kSetup) {
                 if ((int32_t)bounce >= p.depth) {
@@ -664,7 +733,8 @@ __attribute__((amdgpu_waves_per_eu(RT_WAVES_PER_EU, 8))) void trace_kernel(Trace
                     const bool cam = bounce == 0 && p.cam_nnodes != 0;
                     if (tri_begin(p, org, dir, best_t, cam, e, tri_t, tri_i, tri_in, tri_done)) {
                         if (cam && p.ptl_off != nullptr) {
-                            tri_primary_list(p, slot, org, dir, best_t, tri_t, tri_i, tri_in, tri_done);
+                            tri_primary_list(p, lane_job(slot), org, dir, best_t, tri_t, tri_i, tri_in,
+                                             tri_done);
                         } else {
                             node = 0;
                             phase = kTri;
@@ -769,17 +839,43 @@ __attribute__((amdgpu_waves_per_eu(RT_WAVES_PER_EU, 8))) void trace_kernel(Trace
             }
             RT_STAMP(3);
             if (done) {
-                // planar slab (R, G, B planes of njobs floats): 12 B per sample
-                p.samples[slot] = out_r;
-                p.samples[(size_t)p.njobs + slot] = out_g;
-                p.samples[2 * (size_t)p.njobs + slot] = out_b;
+                // planar (R, G, B planes): 12 B per sample, to the slab or the ring
+                sbase[slot] = out_r;
+                sbase[pstride + slot] = out_g;
+                sbase[2 * pstride + slot] = out_b;
                 active = false;
             }
         }
-        // ---- refill lanes whose path ended (active-ray compaction) -------
         const uint64_t dead = __ballot(!active);
         const uint32_t ndead = (uint32_t)__popcll(dead);
-        if (dead != 0 && !exhausted && (ndead >= p.refill_min || ndead == kWave)) {
+        const bool refill = dead != 0 && (ndead >= p.refill_min || ndead == kWave);
+        // ---- fused resolve, at refill points: lanes that finished since the
+        // last one (slot != ~0) are counted against their chunk's ring slot; a
+        // chunk with no samples left is summed now, by this wave, while its
+        // samples are still in the cache.  (Every lane is idle in the last
+        // iteration, so every chunk is resolved before the wave exits.)
+        if (fused && refill) {
+            const bool fin = !active && slot != ~0u;
+            if (__ballot(fin) != 0) {
+                const uint32_t lk = slot >> p.ring_shift;
+#pragma unroll
+                for (uint32_t k = 0; k < kTraceRing; ++k) {
+                    if (rfree & (1u << k)) continue;
+                    const uint32_t n = (uint32_t)__popcll(__ballot(fin && lk == k));
+                    rleft[k] -= n;
+                    if (n != 0 && rleft[k] == 0) {
+                        if (!(p.ablate & 2u))
+                            resolve_chunk(p, sbase, pstride, k << p.ring_shift, rbase[k], rlen[k], lane);
+                        rfree |= 1u << k;
+                    }
+                }
+                if (fin) slot = ~0u;
+            }
+        }
+        // ---- refill lanes whose path ended (active-ray compaction) -------
+        // (with the fused resolve a new chunk needs a free ring slot: with all
+        // kTraceRing slots waiting on unfinished samples the lanes stay idle)
+        if (refill && !exhausted && !(fused && rfree == 0 && pool_next >= pool_end)) {
             if (pool_next >= pool_end) {
                 uint32_t base = 0;
                 if (lane == 0) {
@@ -803,6 +899,14 @@ __attribute__((amdgpu_waves_per_eu(RT_WAVES_PER_EU, 8))) void trace_kernel(Trace
                 } else {
                     pool_next = base;
                     pool_end = min(base + p.chunk, pend);
+                    if (fused) {
+                        const uint32_t k = (uint32_t)__builtin_ctz(rfree);
+                        rfree &= ~(1u << k);
+#pragma unroll
+                        for (uint32_t i = 0; i < kTraceRing; ++i)
+                            if (i == k) rbase[i] = base, rlen[i] = rleft[i] = pool_end - base;
+                        cur_off = (k << p.ring_shift) - base;
+                    }
                 }
             }
             const uint32_t avail = pool_end - pool_next;
@@ -819,7 +923,7 @@ __attribute__((amdgpu_waves_per_eu(RT_WAVES_PER_EU, 8))) void trace_kernel(Trace
                 // enumeration order changes no bits.
                 uint32_t s, col, row;
                 job_pixel(p, job, s, col, row);
-                slot = job;
+                slot = job + cur_off;
                 const uint64_t gjob = ((uint64_t)row * p.width + col) * p.spp + s;
                 rng = (p.mode == kRngReplay) ? p.replay[gjob] : counter_seed(p.seed, gjob);
                 // common.rs:335-337: u drawn before v; camera.rs:84-89

@@ -1,10 +1,12 @@
 // runtime.cpp -- frame driver of the HIP render path (host side).
 //
 // Owns each world's device-resident scene (uploaded once per device, reused
-// by every frame and every camera move), the per-sample slab and the launch
-// sequence: for every slab of tile rows, zero the job counter, launch the
-// persistent trace kernel, then the ordered resolve kernel.  The reference's
-// equivalent is ray_trace's triple loop (common.rs:320-361).
+// by every frame and every camera move), the per-wave sample rings (or the
+// per-sample slab) and the launch sequence: for every launch of tile rows,
+// zero the job counters and launch the persistent trace kernel, which
+// resolves pixels itself; with RT_FLAG_KEEP_SAMPLES the samples go to the
+// slab and the ordered resolve kernel follows.  The reference's equivalent is
+// ray_trace's triple loop (common.rs:320-361).
 #include "runtime.h"
 
 #include <algorithm>
@@ -43,7 +45,7 @@ const std::string &last_error() { return g_error; }
 DeviceState::~DeviceState() {
     if (device < 0) return;
     if (hipSetDevice(device) != hipSuccess) return;
-    void *bufs[] = {sph_hot, sph_cold, tri_hot, tri_geo, mats, samples, out, replay, counter, stats,
+    void *bufs[] = {sph_hot, sph_cold, tri_hot, tri_geo, mats, samples, ring, out, replay, counter, stats,
                     bvh_nodes, bvh_prims, big_hot, bvh_miss, bvh_prim_id, big_id, bvh_miss16,
                     sph_shade, sph_kind, tbvh_nodes, tbvh_tris, tbvh_loose,
                     cam_nodes, cam_tris, ptl_off, ptl_items};
@@ -241,10 +243,18 @@ int render_frame(WorldState &w, const CameraModel &cam, size_t width, size_t hei
     const uint32_t spp = o.samples_per_pixel > 0 ? (uint32_t)o.samples_per_pixel : 0u;
     const uint64_t jobs_per_row = (uint64_t)width * spp;
     if (jobs_per_row > 0x7FFFFFFFull) { set_error("width*spp too large"); return -1; }
-    const uint64_t slab_jobs = env_u64("RT_AMD_SLAB_JOBS", 1ull << 30);  // 16 GB of slab at most
+    // Fused resolve (default): samples live in per-wave rings and the trace
+    // kernel writes the RGBA8 pixels.  The slab path (every sample to HBM, then
+    // resolve_kernel) serves RT_FLAG_KEEP_SAMPLES and spp above 4096 (a ring
+    // slot holds at least one whole pixel).
+    const bool fused = spp > 0 && spp <= 4096 && !(o.flags & RT_FLAG_KEEP_SAMPLES) &&
+                       env_u64("RT_AMD_FUSED", 1) != 0;
+    // jobs per launch: 2^31 (fused: C3 in one launch) or 2^30 (a 12 GB slab)
+    const uint64_t slab_jobs = env_u64("RT_AMD_SLAB_JOBS", fused ? (1ull << 31) - 1 : 1ull << 30);
     size_t rows_per_slab = jobs_per_row ? (size_t)std::max<uint64_t>(1, slab_jobs / jobs_per_row) : T;
     rows_per_slab = std::min(rows_per_slab, T);
-    if (jobs_per_row) HIP_TRY(grow(d->samples, d->samples_cap, 3 * rows_per_slab * jobs_per_row));
+    if (jobs_per_row && !fused)
+        HIP_TRY(grow(d->samples, d->samples_cap, 3 * rows_per_slab * jobs_per_row));
 
     if (o.rng_mode == RT_RNG_REPLAY && spp) {
         const size_t n = width * height * (size_t)spp;
@@ -362,6 +372,16 @@ int render_frame(WorldState &w, const CameraModel &cam, size_t width, size_t hei
         p.tbvh_r = tb.radius; p.tbvh_mag = tb.mag;
     }
     const float inv_spp = 1.0f / (float)o.samples_per_pixel;  // 1.0 / spp as f32 (common.rs:345)
+    p.inv_spp = inv_spp;
+    {
+        // every sample's alpha is exactly 1.0, so each pixel's
+        // alpha byte is this one fold, done once (resolve_kernel does it per pixel)
+        float a = 1.0f;  // Color::new(0,0,0) has alpha 1 (color.rs:21-23)
+        for (uint32_t k = 0; k < spp && a + 1.0f != a; ++k) a = a + 1.0f;
+        const float x = a * inv_spp * 255.999f;
+        p.alpha_u8 = !(x > 0.0f) ? 0u : x >= 255.0f ? 255u : (uint32_t)x;  // saturating `as u8`
+    }
+    p.out = d_out;
 
     // sliced walks pay off when walk lengths vary a lot: scenes with a triangle tree
     p.step = (uint32_t)env_u64("RT_AMD_STEP", use_tbvh ? 1 : 0) != 0;
@@ -391,21 +411,43 @@ int render_frame(WorldState &w, const CameraModel &cam, size_t width, size_t hei
             const uint64_t nwaves = blocks * waves_per_block;
             uint64_t chunk = env_u64("RT_AMD_CHUNK", 0);
             if (!chunk) chunk = std::min<uint64_t>(256, std::max<uint64_t>(64, njobs / (nwaves * 16) / 64 * 64));
+            // whole pixels per chunk (partitions are pixel-aligned too), so a
+            // chunk's pixels are complete once its samples are
+            chunk = chunk >= spp ? chunk / spp * spp : spp;
+            if (fused) {
+                // a resolve sums one pixel per lane, so whole-walk kernels take
+                // chunks of >= 8 pixels (<= 4096 jobs unless spp is larger;
+                // A/B, C2: 4 px 7.10 ms, 8 px 6.79, 16 px 6.83, 32 px 7.36,
+                // slab + resolve_kernel 6.94).  Sliced walks keep their chunk
+                // (C5: 16 px +1.5 %, 4 px = slab)
+                const uint64_t px = std::max<uint64_t>(1, std::min<uint64_t>(
+                    env_u64("RT_AMD_RESOLVE_PIX", p.step ? 1 : 8), 4096 / spp));
+                chunk = std::max<uint64_t>(chunk, px * spp);
+            }
             p.chunk = (uint32_t)chunk;
+            p.ring = nullptr;
+            p.ring_shift = 0;
+            if (fused) {
+                while ((1ull << p.ring_shift) < chunk) ++p.ring_shift;
+                HIP_TRY(grow(d->ring, d->ring_cap, nwaves * 3 * (kTraceRing << p.ring_shift)));
+                p.ring = d->ring;
+            }
             // job-queue partitions: each keeps >= 16 chunks
             uint64_t parts = env_u64("RT_AMD_PARTS", 64);
             parts = std::max<uint64_t>(1, std::min<uint64_t>({parts, kMaxParts, njobs / (16 * chunk) + 1}));
             p.nparts = (uint32_t)parts;
             HIP_TRY(hipMemsetAsync(d->counter, 0, parts * 128, s));
             HIP_TRY(launch_trace(p, (uint32_t)blocks, s));
-            d->last_jobs = njobs;
+            d->last_jobs = fused ? 0 : njobs;
             d->last_spp = spp;
+            d->last_fused = fused;  // rt_read_samples needs the slab
             ++launches;
             waves = (uint32_t)nwaves;
         }
         if (timed) HIP_TRY(hipEventRecord(d->ev[1], s));
-        HIP_TRY(launch_resolve_ex(d->samples, d_out, (uint32_t)(rows * width), spp, inv_spp,
-                                  (uint32_t)width, (uint32_t)r0, s));
+        if (!fused)  // (spp 0: no samples, the resolve still writes every pixel)
+            HIP_TRY(launch_resolve_ex(d->samples, d_out, (uint32_t)(rows * width), spp, inv_spp,
+                                      (uint32_t)width, (uint32_t)r0, s));
         if (timed) {
             HIP_TRY(hipEventRecord(d->ev[2], s));
             HIP_TRY(hipEventSynchronize(d->ev[2]));
@@ -438,6 +480,7 @@ int render_frame(WorldState &w, const CameraModel &cam, size_t width, size_t hei
         for (int k = 0; k < 4; ++k) stats->stamp_cycles[k] = st[4 + k];
         stats->tri_node_tests = st[8];
         stats->tri_bvh = use_tbvh ? 1u : 0u;
+        stats->fused_resolve = fused ? 1u : 0u;
         stats->bvh_tri_tests = use_tbvh ? st[9] : stats->tri_tests;
     }
     return 0;
@@ -447,6 +490,11 @@ long read_samples(WorldState &w, int device, float *out, size_t n) {
     DeviceState *d = nullptr;
     int rc = device_for(w, device, d);
     if (rc) return rc;
+    if (d->last_fused) {
+        set_error("rt_read_samples: the last launch resolved in the trace kernel "
+                  "(render with RT_FLAG_KEEP_SAMPLES to keep the samples)");
+        return -1;
+    }
     const size_t count = std::min(n / 4, d->last_jobs);
     if (!count) return 0;
     HIP_TRY(hipDeviceSynchronize());

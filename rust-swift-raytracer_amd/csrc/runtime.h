@@ -47,6 +47,7 @@ struct DeviceState {
     uint64_t ptl_version = 0;
     size_t lds_bytes = 0;                                       // 0: tree not LDS-stageable
     float *samples = nullptr;        size_t samples_cap = 0;   // sample slab (3 planes)
+    float *ring = nullptr;           size_t ring_cap = 0;      // per-wave sample rings (fused resolve)
     uint32_t *out = nullptr;         size_t out_cap = 0;       // RGBA8 tile (host path)
     uint32_t *replay = nullptr;      size_t replay_cap = 0;
     uint32_t *counter = nullptr;                                // job counter
@@ -56,6 +57,7 @@ struct DeviceState {
     int num_cus = 0;
     size_t last_jobs = 0;                                       // jobs of the last launch
     size_t last_spp = 0;                                        // and its spp
+    bool last_fused = false;                                    // it resolved in-kernel (no slab)
     ~DeviceState();
 };
 

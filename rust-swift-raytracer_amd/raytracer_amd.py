@@ -19,6 +19,7 @@ LIB_PATH = os.path.join(HERE, "lib", "libraytracer.so")
 
 RNG_COUNTER, RNG_REPLAY = 1, 2
 ACCEL_AUTO, ACCEL_BRUTE, ACCEL_BVH = 0, 1, 2
+FLAG_KEEP_SAMPLES = 1
 DEFAULT_SEED = 2547549
 
 # Every symbol declared in include/raytracer.h and include/raytracer_amd.h.
@@ -52,7 +53,7 @@ class RenderOptions(C.Structure):
                 ("rng_mode", C.c_uint32), ("seed", C.c_uint32),
                 ("replay_states", C.POINTER(C.c_uint32)), ("row_block", C.c_uint32),
                 ("rank", C.c_uint32), ("nranks", C.c_uint32), ("device", C.c_int32),
-                ("accel", C.c_int32)]
+                ("accel", C.c_int32), ("flags", C.c_uint32)]
 
 
 class RenderStats(C.Structure):
@@ -63,7 +64,7 @@ class RenderStats(C.Structure):
                 ("bvh_sphere_tests", C.c_uint64), ("bvh_node_tests", C.c_uint64),
                 ("big_sphere_tests", C.c_uint64), ("stamp_cycles", C.c_uint64 * 4),
                 ("tri_node_tests", C.c_uint64), ("bvh_tri_tests", C.c_uint64),
-                ("tri_bvh", C.c_uint32), ("reserved", C.c_uint32)]
+                ("tri_bvh", C.c_uint32), ("fused_resolve", C.c_uint32)]
 
     def as_dict(self):
         out = {}
@@ -150,12 +151,13 @@ def sample_seed(seed: int, job: int) -> int:
 
 
 def options(spp=16, depth=8, mode=RNG_COUNTER, seed=DEFAULT_SEED, replay=None, row_block=1,
-            rank=0, nranks=1, device=-1, accel=ACCEL_AUTO, L=None):
+            rank=0, nranks=1, device=-1, accel=ACCEL_AUTO, keep_samples=False, L=None):
     o = RenderOptions()
     (L or lib()).rt_default_options(C.byref(o))
     o.samples_per_pixel, o.max_ray_bounces, o.rng_mode, o.seed = spp, depth, mode, seed
     o.row_block, o.rank, o.nranks, o.device = row_block, rank, nranks, device
     o.accel = accel
+    o.flags = FLAG_KEEP_SAMPLES if keep_samples else 0
     keep = None
     if replay is not None:
         keep = np.ascontiguousarray(replay, dtype=np.uint32)
@@ -228,10 +230,13 @@ class World:
         return px
 
     def render(self, width, height, spp=16, depth=8, mode=RNG_COUNTER, seed=DEFAULT_SEED,
-               replay=None, row_block=1, rank=0, nranks=1, device=-1, accel=ACCEL_AUTO):
-        """rt_render_ex -> (rgba uint8[tile_rows, width, 4], stats dict)."""
+               replay=None, row_block=1, rank=0, nranks=1, device=-1, accel=ACCEL_AUTO,
+               keep_samples=False):
+        """rt_render_ex -> (rgba uint8[tile_rows, width, 4], stats dict).
+        keep_samples: write every sample to the slab (for read_samples) and
+        resolve with the second kernel; the frame is bit-identical."""
         o, keep = options(spp, depth, mode, seed, replay, row_block, rank, nranks, device, accel,
-                          self._L)
+                          keep_samples, self._L)
         rows = int(self._L.rt_tile_rows(height, row_block, rank, nranks)) if nranks > 1 else height
         px = np.zeros((rows, width, 4), np.uint8)
         fb = CFramebuffer(width, height, px.ctypes.data_as(C.POINTER(ColorU8)))
@@ -253,11 +258,12 @@ class World:
 
     def render_device(self, width, height, out_ptr: int, stream_ptr: int = 0, spp=16, depth=8,
                       mode=RNG_COUNTER, seed=DEFAULT_SEED, row_block=1, rank=0, nranks=1,
-                      device=-1, accel=ACCEL_AUTO, stats=True):
+                      device=-1, accel=ACCEL_AUTO, stats=True, keep_samples=False):
         """rt_render_device into a device buffer (e.g. a torch uint8 tensor).
         stats=False: no counters and no host wait -- the frame is only enqueued
         on the stream (returns None)."""
-        o, _ = options(spp, depth, mode, seed, None, row_block, rank, nranks, device, accel, self._L)
+        o, _ = options(spp, depth, mode, seed, None, row_block, rank, nranks, device, accel,
+                       keep_samples, self._L)
         st = RenderStats()
         rc = self._L.rt_render_device(self._h, width, height, C.byref(o), C.c_void_p(out_ptr),
                                     C.c_void_p(stream_ptr or None), C.byref(st) if stats else None)

@@ -41,6 +41,18 @@ def assert_bits_equal(a, b, what):
     assert bad.size == 0, f"{what}: {len(bad)} mismatches, first at {bad[:5].tolist()}"
 
 
+def render_kept(world, *args, **kw):
+    """Renders twice: by default (pixels resolved inside the trace kernel from
+    per-wave sample rings) and with keep_samples (every sample to the slab,
+    then resolve_kernel).  Both frames must agree bit for bit; afterwards the
+    samples are readable (world.read_samples)."""
+    out, st = world.render(*args, **kw)
+    kept, st2 = world.render(*args, keep_samples=True, **kw)
+    assert_bits_equal(kept, out, "in-kernel resolve vs slab + resolve kernel")
+    assert st2["rays"] == st["rays"]
+    return out, st
+
+
 @pytest.mark.parametrize("scene,w,h,spp,depth", [
     (CWORLD, 40, 30, 4, 8),
     ("world.txt", 33, 17, 3, 8),
@@ -52,7 +64,7 @@ def test_replay_matches_reference_serial(scene, w, h, spp, depth):
     img, st, states, smp = ref.render(w, h, spp, depth, mode=O.RNG_SERIAL, record_states=True,
                                       record_samples=True)
     world = R.World(src)
-    out, gst = world.render(w, h, spp, depth, mode=R.RNG_REPLAY, replay=states)
+    out, gst = render_kept(world, w, h, spp, depth, mode=R.RNG_REPLAY, replay=states)
     assert_bits_equal(out, img, "frame")
     assert_bits_equal(world.read_samples(w * h * spp)[:, :3],
                       oracle_samples_to_gpu_order(smp, w, h, spp)[:, :3], "samples")
@@ -90,7 +102,7 @@ def test_counter_mode_bit_exact(scene, w, h, spp, depth, seed):
     img, st, _, smp = O.Scene(src).render(w, h, spp, depth, mode=O.RNG_COUNTER, seed=seed,
                                           nthreads=8, record_samples=True)
     world = R.World(src)
-    out, gst = world.render(w, h, spp, depth, mode=R.RNG_COUNTER, seed=seed)
+    out, gst = render_kept(world, w, h, spp, depth, mode=R.RNG_COUNTER, seed=seed)
     assert_bits_equal(out, img, "frame")
     assert_bits_equal(world.read_samples(w * h * spp)[:, :3],
                       oracle_samples_to_gpu_order(smp, w, h, spp)[:, :3], "samples")
@@ -137,6 +149,28 @@ def test_edge_cases(w, h, spp, depth):
     assert gst["rays"] == st["rays"]
 
 
+@pytest.mark.parametrize("spp", [1, 3, 64, 255, 257, 1000, 4097])
+def test_in_kernel_resolve_chunking(spp):
+    """Chunk and ring geometry of the in-kernel resolve: spp below, at and
+    above the 256-job chunk (1000: one pixel per 1024-sample ring slot) and
+    above 4096 (the slab path): bit-exact against the oracle."""
+    src = scene_text("rtow.txt")
+    w, h = (24, 8) if spp < 1000 else (5, 3)
+    img, st, _ = O.Scene(src).render(w, h, spp, 8, mode=O.RNG_COUNTER, nthreads=8)
+    world = R.World(src)
+    out, gst = world.render(w, h, spp, 8)
+    assert_bits_equal(out, img, f"frame spp {spp}")
+    assert gst["rays"] == st["rays"]
+    assert gst["fused_resolve"] == (1 if spp <= 4096 else 0)
+
+
+def test_read_samples_needs_keep_samples():
+    world = R.World(scene_text(CWORLD))
+    world.render(16, 8, 4, 8)
+    with pytest.raises(R.RenderError, match="KEEP_SAMPLES"):
+        world.read_samples(16 * 8 * 4)
+
+
 def test_empty_and_triangle_only_scenes():
     for src in ["camera origin 0.0 0.0 0.0 aspect 1.5;",
                 "camera origin 0.0 0.5 0.0 aspect 1.0;\nmaterial M : Metal color 0.9 0.2 0.2 fuzz 0.1;\n"
@@ -159,7 +193,7 @@ def test_mesh_scene_triangle_path():
     out, gst = world.render(w, h, spp, 8, mode=R.RNG_COUNTER, accel=R.ACCEL_BRUTE)
     assert_bits_equal(out, img, "mesh frame (brute force)")
     assert gst["rays"] == st["rays"] and gst["tri_in_range"] == st["tri_in_range"]
-    out, gst = world.render(w, h, spp, 8, mode=R.RNG_COUNTER)
+    out, gst = render_kept(world, w, h, spp, 8, mode=R.RNG_COUNTER)
     assert gst["tri_bvh"] == 1
     assert_bits_equal(out, img, "mesh frame (BVH)")
     assert_bits_equal(world.read_samples(w * h * spp)[:, :3],
@@ -216,7 +250,7 @@ def test_scheduling_knobs_do_not_change_samples(monkeypatch, scene):
     src = scene_text("rtow.txt") if scene == "rtow" else _triangle_scene(41, 400, spheres=40)
     w, h, spp = 160, 90, 4
     world = R.World(src)
-    ref, _ = world.render(w, h, spp, 8)
+    ref, _ = render_kept(world, w, h, spp, 8)
     ref_s = world.read_samples(w * h * spp)
     for env in [dict(RT_AMD_PARTS="1"), dict(RT_AMD_PARTS="7", RT_AMD_CHUNK="64"),
                 dict(RT_AMD_PARTS="1024"), dict(RT_AMD_STEP="1", RT_AMD_STEPS="1"),
@@ -226,7 +260,7 @@ def test_scheduling_knobs_do_not_change_samples(monkeypatch, scene):
                 dict(RT_AMD_LINEAR_E="1"), dict(RT_AMD_PRIMARY_LISTS="0")]:
         for k, v in env.items():
             monkeypatch.setenv(k, v)
-        out, _ = world.render(w, h, spp, 8)
+        out, _ = render_kept(world, w, h, spp, 8)
         assert_bits_equal(out, ref, f"frame {env}")
         assert_bits_equal(world.read_samples(w * h * spp), ref_s, f"samples {env}")
         for k in env:
@@ -243,6 +277,9 @@ def test_full_size_c2_properties():
     assert_bits_equal(a, b, "determinism")
     assert st["rays"] == st2["rays"] and st["samples"] == W * H * spp
     assert (a[..., 3] == 255).all()
+    c, st3 = world.render(W, H, spp, depth, keep_samples=True)  # 1.6 GB slab + resolve_kernel
+    assert_bits_equal(c, a, "in-kernel resolve vs slab + resolve kernel")
+    assert st3["rays"] == st["rays"] and st["fused_resolve"] == 1 and st3["fused_resolve"] == 0
     ref = O.Scene(src)
     rows = [0, 333, 700, 1079]  # reference rows (0 = bottom)
     img = np.zeros((H, W, 4), np.uint8)
@@ -275,9 +312,9 @@ def _random_scene(seed, n, spread, radius, offset=(0.0, 0.0, 0.0), dup=0, big=Tr
 
 def _both_modes(src, w, h, spp, depth=8):
     world = R.World(src)
-    a, sa = world.render(w, h, spp, depth, accel=R.ACCEL_BRUTE)
+    a, sa = render_kept(world, w, h, spp, depth, accel=R.ACCEL_BRUTE)
     sma = world.read_samples(w * h * spp)
-    b, sb = world.render(w, h, spp, depth, accel=R.ACCEL_BVH)
+    b, sb = render_kept(world, w, h, spp, depth, accel=R.ACCEL_BVH)
     smb = world.read_samples(w * h * spp)
     return a, sa, sma, b, sb, smb
 
@@ -305,7 +342,7 @@ def test_bvh_matches_oracle_rtow():
     img, st, _, smp = O.Scene(src).render(64, 36, 4, 8, mode=O.RNG_COUNTER, nthreads=8,
                                           record_samples=True)
     world = R.World(src)
-    out, gst = world.render(64, 36, 4, 8, accel=R.ACCEL_BVH)
+    out, gst = render_kept(world, 64, 36, 4, 8, accel=R.ACCEL_BVH)
     assert gst["accel"] == R.ACCEL_BVH
     assert_bits_equal(out, img, "frame")
     assert_bits_equal(world.read_samples(64 * 36 * 4)[:, :3],
@@ -349,7 +386,7 @@ def test_triangle_bvh_matches_oracle():
     img, st, _, smp = O.Scene(src).render(48, 32, 4, 8, mode=O.RNG_COUNTER, nthreads=8,
                                           record_samples=True)
     world = R.World(src)
-    out, gst = world.render(48, 32, 4, 8)
+    out, gst = render_kept(world, 48, 32, 4, 8)
     assert gst["tri_bvh"] == 1
     assert_bits_equal(out, img, "frame")
     assert_bits_equal(world.read_samples(48 * 32 * 4)[:, :3],
@@ -372,9 +409,9 @@ def test_triangle_camera_tree_follows_camera_moves():
     world = R.World(src)
     for mv in [(0.0, 0.0, 0.0), (0.5, -0.25, 1.0), (-3.0, 2.0, -4.0), (0.0, 0.0, 0.0)]:
         world.move_camera(*mv)
-        a, sa = world.render(64, 48, 4, 8, accel=R.ACCEL_BRUTE)
+        a, sa = render_kept(world, 64, 48, 4, 8, accel=R.ACCEL_BRUTE)
         sma = world.read_samples(64 * 48 * 4)
-        b, sb = world.render(64, 48, 4, 8, accel=R.ACCEL_BVH)
+        b, sb = render_kept(world, 64, 48, 4, 8, accel=R.ACCEL_BVH)
         smb = world.read_samples(64 * 48 * 4)
         assert sb["tri_bvh"] == 1
         assert_bits_equal(b, a, f"frame after move {mv}")
@@ -392,9 +429,9 @@ def test_primary_triangle_lists_follow_camera_and_size():
                        ((0.3, -0.2, -5.0), (120, 80)), ((0.0, 1.5, -9.0), (64, 150)),
                        ((-2.0, 0.0, 12.0), (80, 45))]:
         world.move_camera(*mv)
-        a, _ = world.render(w, h, 4, 8, accel=R.ACCEL_BRUTE)
+        a, _ = render_kept(world, w, h, 4, 8, accel=R.ACCEL_BRUTE)
         sa = world.read_samples(w * h * 4)
-        b, sb = world.render(w, h, 4, 8, accel=R.ACCEL_BVH)
+        b, sb = render_kept(world, w, h, 4, 8, accel=R.ACCEL_BVH)
         smb = world.read_samples(w * h * 4)
         assert sb["tri_bvh"] == 1
         assert_bits_equal(b, a, f"frame {mv} {w}x{h}")
