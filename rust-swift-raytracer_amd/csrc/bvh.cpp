@@ -574,6 +574,104 @@ SphereBVH build_sphere_bvh(const std::vector<Sphere> &spheres, uint32_t leaf_siz
 
 namespace rtamd {
 
+// Inverse of the camera map: a primary ray's direction is M (u, v, 1) with
+// M = [h | v | llc - o] (camera.rs:84-89), so a point P - o maps to w = Mi (P - o)
+// and lies on the ray of (u, v) = (w0 / w2, w1 / w2) when w2 > 0.
+static bool camera_inverse(const CameraModel &cam, double Mi[3][3]) {
+    double M[3][3];
+    const Vec3 cols[3] = {cam.horizontal, cam.vertical, {cam.lower_left.x - cam.origin.x,
+                                                         cam.lower_left.y - cam.origin.y,
+                                                         cam.lower_left.z - cam.origin.z}};
+    for (int j = 0; j < 3; ++j) { M[0][j] = cols[j].x; M[1][j] = cols[j].y; M[2][j] = cols[j].z; }
+    const double det = M[0][0] * (M[1][1] * M[2][2] - M[1][2] * M[2][1]) -
+                       M[0][1] * (M[1][0] * M[2][2] - M[1][2] * M[2][0]) +
+                       M[0][2] * (M[1][0] * M[2][1] - M[1][1] * M[2][0]);
+    if (!(std::fabs(det) > 0) || !std::isfinite(det)) return false;
+    Mi[0][0] = (M[1][1] * M[2][2] - M[1][2] * M[2][1]) / det;
+    Mi[0][1] = (M[0][2] * M[2][1] - M[0][1] * M[2][2]) / det;
+    Mi[0][2] = (M[0][1] * M[1][2] - M[0][2] * M[1][1]) / det;
+    Mi[1][0] = (M[1][2] * M[2][0] - M[1][0] * M[2][2]) / det;
+    Mi[1][1] = (M[0][0] * M[2][2] - M[0][2] * M[2][0]) / det;
+    Mi[1][2] = (M[0][2] * M[1][0] - M[0][0] * M[1][2]) / det;
+    Mi[2][0] = (M[1][0] * M[2][1] - M[1][1] * M[2][0]) / det;
+    Mi[2][1] = (M[0][1] * M[2][0] - M[0][0] * M[2][1]) / det;
+    Mi[2][2] = (M[0][0] * M[1][1] - M[0][1] * M[1][0]) / det;
+    return true;
+}
+
+PrimarySphereLists build_primary_sphere_lists(const SphereBVH &bv, const CameraModel &cam,
+                                              size_t width, size_t height) {
+    PrimarySphereLists out;
+    const size_t n = bv.prims.size() / 4;
+    if (n == 0 || n >= kSphListWalk || width < 2 || height < 2 || height > (1u << 24) ||
+        width > (1u << 24) || width * height > (1ull << 28))
+        return out;
+    // the one-pixel margins below cover the rounding of u, v and the ray
+    // direction (relative ~1e-7 of the camera's coordinates) for cameras near
+    // the scene's scale; far-off cameras walk the tree instead
+    const Vec3 cv[4] = {cam.origin, cam.lower_left, cam.horizontal, cam.vertical};
+    double mag = 0;
+    for (const Vec3 &v : cv) mag = std::max({mag, std::fabs((double)v.x), std::fabs((double)v.y),
+                                             std::fabs((double)v.z)});
+    double Mi[3][3];
+    if (!(mag < 1e3) || !camera_inverse(cam, Mi)) return out;
+    const double o[3] = {cam.origin.x, cam.origin.y, cam.origin.z};
+    const double e_abs = 4e-6 * (std::fabs(o[0]) + std::fabs(o[1]) + std::fabs(o[2]) + bv.mag);
+    const double wden = (double)(float)(width - 1), hden = (double)(float)(height - 1);
+    const int64_t W = (int64_t)width, H = (int64_t)height;
+    std::vector<uint8_t> cnt(width * height, 0);  // kSphListMax + 1 = overflow
+    out.rec.assign(2 * width * height, 0);
+    for (uint32_t i = 0; i < n; ++i) {
+        const float *s = &bv.prims[(size_t)i * 4];
+        const double c[3] = {s[0], s[1], s[2]};
+        const double r = std::sqrt((double)s[3]) * (1 + 1e-6);
+        const double a = std::sqrt((c[0] - o[0]) * (c[0] - o[0]) + (c[1] - o[1]) * (c[1] - o[1]) +
+                                   (c[2] - o[2]) * (c[2] - o[2]));
+        // the walk's margin (render.hip sph_inflation, K = 3e-3), doubled
+        const double R = r + 2 * 3e-3 * (a + r) * 1.01 + 2 * e_abs;
+        if (!std::isfinite(R) || !std::isfinite(a)) return PrimarySphereLists{};
+        double umin = 1e300, umax = -1e300, vmin = 1e300, vmax = -1e300;
+        int front = 0, behind = 0;
+        for (int k = 0; k < 8; ++k) {  // corners of the inflated ball's box
+            const double P[3] = {c[0] + (k & 1 ? R : -R) - o[0], c[1] + (k & 2 ? R : -R) - o[1],
+                                 c[2] + (k & 4 ? R : -R) - o[2]};
+            double w[3];
+            for (int q = 0; q < 3; ++q) w[q] = Mi[q][0] * P[0] + Mi[q][1] * P[1] + Mi[q][2] * P[2];
+            const double wn = std::fabs(w[0]) + std::fabs(w[1]) + std::fabs(w[2]);
+            if (w[2] > 1e-6 * wn) {
+                ++front;
+                umin = std::min(umin, w[0] / w[2]); umax = std::max(umax, w[0] / w[2]);
+                vmin = std::min(vmin, w[1] / w[2]); vmax = std::max(vmax, w[1] / w[2]);
+            } else if (w[2] < -1e-6 * wn) {
+                ++behind;
+            }
+        }
+        if (behind == 8) continue;                         // no point of positive depth
+        if (front < 8) return PrimarySphereLists{};        // straddles the camera plane: walk
+        // pixel col covers u in [col, col + 1] / wden; one pixel of margin each side
+        const double cl = std::floor(umin * wden) - 2, ch = std::floor(umax * wden) + 1;
+        const double rl = std::floor(vmin * hden) - 2, rh = std::floor(vmax * hden) + 1;
+        if (ch < 0 || cl > (double)(W - 1) || rh < 0 || rl > (double)(H - 1)) continue;
+        const int64_t c0 = std::max<int64_t>(0, (int64_t)cl), c1 = std::min<int64_t>(W - 1, (int64_t)ch);
+        const int64_t r0 = std::max<int64_t>(0, (int64_t)rl), r1 = std::min<int64_t>(H - 1, (int64_t)rh);
+        for (int64_t rb = r0; rb <= r1; ++rb) {  // rb counts from the bottom (common.rs:327)
+            const size_t row = (size_t)(H - 1 - rb) * width;
+            for (int64_t col = c0; col <= c1; ++col) {
+                const size_t px = row + (size_t)col;
+                const uint32_t k = cnt[px];
+                if (k >= kSphListMax) { cnt[px] = kSphListMax + 1; continue; }
+                uint32_t &word = out.rec[2 * px + (k >> 1)];
+                word |= i << (16 * (k & 1));
+                cnt[px] = (uint8_t)(k + 1);
+            }
+        }
+    }
+    for (size_t px = 0; px < width * height; ++px)
+        out.rec[2 * px + 1] = (out.rec[2 * px + 1] & 0xFFFFu) |
+                              ((cnt[px] > kSphListMax ? kSphListWalk : cnt[px]) << 16);
+    return out;
+}
+
 PrimaryTriLists build_primary_tri_lists(const CameraTriangleBVH &ct, const CameraModel &cam,
                                         size_t width, size_t height) {
     PrimaryTriLists out;

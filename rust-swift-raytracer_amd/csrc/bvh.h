@@ -123,4 +123,23 @@ struct PrimaryTriLists {
 PrimaryTriLists build_primary_tri_lists(const CameraTriangleBVH &ct, const CameraModel &cam,
                                         size_t width, size_t height);
 
+// Primary-ray sphere candidates (bounce 0, instead of the sphere-tree walk).
+// A primary ray of pixel (col, row) points into that pixel's footprint, so
+// only tree spheres whose inflated ball (radius r + K(|o - c| + r) + e_abs, the
+// walk's pruning margin) projects onto the footprint can produce
+// a candidate.  Each pixel keeps up to kSphListMax such spheres (tree-order
+// prim indices); a pixel with more, and every pixel when some ball is not
+// entirely in front of the camera, walks the tree instead.  Balls entirely
+// behind the camera are dropped.  Candidates keep the (t, index) argmin, so
+// the order of the list does not matter (bvh.h header).
+constexpr uint32_t kSphListMax = 3;
+constexpr uint32_t kSphListWalk = 0xFFFFu;
+struct PrimarySphereLists {
+    // 2 u32 per image pixel (row 0 = top): (i0 | i1 << 16, i2 | count << 16),
+    // count in [0, kSphListMax] or kSphListWalk; empty = lists not usable
+    std::vector<uint32_t> rec;
+};
+PrimarySphereLists build_primary_sphere_lists(const SphereBVH &bv, const CameraModel &cam,
+                                              size_t width, size_t height);
+
 }  // namespace rtamd

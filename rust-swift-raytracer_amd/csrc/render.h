@@ -88,6 +88,9 @@ struct TraceParams {
     const uint32_t *ptl_items;
     uint32_t ptl_spr;         // strips per image row
     uint32_t ptl_always, ptl_end;  // items[ptl_always, ptl_end): tested by every primary ray
+    // primary-ray sphere candidates (bvh.h PrimarySphereLists, sphere-only
+    // scenes): per image pixel (i0 | i1 << 16, i2 | count << 16); nullptr: walk
+    const uint2 *spl;
 };
 
 hipError_t launch_trace(const TraceParams &p, uint32_t blocks, hipStream_t stream);

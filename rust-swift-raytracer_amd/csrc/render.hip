@@ -118,6 +118,7 @@ __device__ __forceinline__ uint32_t fdiv(uint32_t n, const FastDiv &f) { return 
 constexpr uint32_t kWave = 64;
 constexpr uint32_t kNodeEndDev = 0xFFFFFFFFu;  // bvh.h kNodeEnd
 constexpr uint32_t kLeafBitDev = 0x80000000u;  // bvh.h kLeafBit
+constexpr uint32_t kSphListWalk = 0xFFFFu;     // bvh.h kSphListWalk
 constexpr uint32_t kBatch = 8;  // spheres per scalar-load batch (sphere count padded to it)
 
 // ------------------------------------------------------------ sphere stage
@@ -515,7 +516,7 @@ __device__ __forceinline__ void resolve_chunk(const TraceParams &p, const float 
         const float *src = ring + off + i * spp;
         float r = 0.0f, g = 0.0f, b = 0.0f;
         if ((spp & 3u) == 0) {
-#pragma unroll 4
+            // (no unrolling: #pragma unroll 4 here spilled the whole kernel)
             for (uint32_t k = 0; k < spp; k += 4) {
                 const float4 R = *reinterpret_cast<const float4 *>(src + k);
                 const float4 G = *reinterpret_cast<const float4 *>(src + plane + k);
@@ -599,6 +600,7 @@ __attribute__((amdgpu_waves_per_eu(RT_WAVES_PER_EU, 8))) void trace_kernel(Trace
     F3 org = f3(0, 0, 0), dir = f3(0, 0, 0), inv = f3(0, 0, 0);
     float thr_r = 1.0f, thr_g = 1.0f, thr_b = 1.0f;  // ray_color's final_color
     uint32_t rng = 0, slot = ~0u, bounce = 0;  // slot ~0: no finished sample to count
+    uint32_t spl0 = 0, spl1 = kSphListWalk << 16;  // the pixel's primary sphere list (p.spl)
     // lane state between loop iterations (see the bounce loop below)
     enum : uint32_t { kSetup = 0, kSph = 1, kTriInit = 2, kTri = 3, kShade = 4 };
     uint32_t phase = kSetup, node = 0, oct = 0;
@@ -699,6 +701,20 @@ __attribute__((amdgpu_waves_per_eu(RT_WAVES_PER_EU, 8))) void trace_kernel(Trace
                         node = 0;
                         // (RT_AMD_ABLATE=1: timing-only diagnostic, results are wrong)
                         phase = (p.ablate & 1u) ? kTriInit : kSph;
+                        if (!kMesh && bounce == 0 && (spl1 >> 16) != kSphListWalk) {
+                            // primary ray: the pixel's candidate spheres instead of
+                            // the walk (bvh.h PrimarySphereLists; same candidate
+                            // arithmetic and (t, index) argmin as sphere_leaf)
+                            const uint32_t nc = spl1 >> 16;
+                            sph_tests += nc;
+                            if (nc > 0) sphere_candidate(view.prims[spl0 & 0xFFFFu], org, dir,
+                                                         (int)view.ids[spl0 & 0xFFFFu], best_t, best_i);
+                            if (nc > 1) sphere_candidate(view.prims[spl0 >> 16], org, dir,
+                                                         (int)view.ids[spl0 >> 16], best_t, best_i);
+                            if (nc > 2) sphere_candidate(view.prims[spl1 & 0xFFFFu], org, dir,
+                                                         (int)view.ids[spl1 & 0xFFFFu], best_t, best_i);
+                            phase = kTriInit;
+                        }
                     } else {
                         spheres_brute(p, org, dir, best_t, best_i);
                         phase = kTriInit;
@@ -924,6 +940,12 @@ __attribute__((amdgpu_waves_per_eu(RT_WAVES_PER_EU, 8))) void trace_kernel(Trace
                 uint32_t s, col, row;
                 job_pixel(p, job, s, col, row);
                 slot = job + cur_off;
+                if (kBvh && !kMesh && p.spl != nullptr) {
+                    // loaded now, used at the ray's setup (next iteration)
+                    const uint2 r = p.spl[(size_t)(p.height - 1u - row) * p.width + col];
+                    spl0 = r.x;
+                    spl1 = r.y;
+                }
                 const uint64_t gjob = ((uint64_t)row * p.width + col) * p.spp + s;
                 rng = (p.mode == kRngReplay) ? p.replay[gjob] : counter_seed(p.seed, gjob);
                 // common.rs:335-337: u drawn before v; camera.rs:84-89

@@ -48,7 +48,7 @@ DeviceState::~DeviceState() {
     void *bufs[] = {sph_hot, sph_cold, tri_hot, tri_geo, mats, samples, ring, out, replay, counter, stats,
                     bvh_nodes, bvh_prims, big_hot, bvh_miss, bvh_prim_id, big_id, bvh_miss16,
                     sph_shade, sph_kind, tbvh_nodes, tbvh_tris, tbvh_loose,
-                    cam_nodes, cam_tris, ptl_off, ptl_items};
+                    cam_nodes, cam_tris, ptl_off, ptl_items, spl};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
     for (hipEvent_t e : ev)
@@ -207,6 +207,18 @@ static void prepare_primary_tri_lists(WorldState &w, const CameraModel &cam, siz
     ++w.ptl_version;
 }
 
+static void prepare_primary_sphere_lists(WorldState &w, const CameraModel &cam, size_t width,
+                                         size_t height) {
+    if (w.spl_version && w.spl_w == width && w.spl_h == height &&
+        std::memcmp(&w.spl_cam, &cam, sizeof(cam)) == 0)
+        return;
+    w.spl = build_primary_sphere_lists(w.bvh, cam, width, height);
+    w.spl_cam = cam;
+    w.spl_w = width;
+    w.spl_h = height;
+    ++w.spl_version;
+}
+
 template <typename T>
 static hipError_t grow(T *&buf, size_t &cap, size_t n) {
     if (n <= cap) return hipSuccess;
@@ -306,6 +318,21 @@ int render_frame(WorldState &w, const CameraModel &cam, size_t width, size_t hei
         for (int k = 0; k < 3; ++k) p.bvh_c[k] = bv.centre[k];
         p.bvh_r = bv.radius; p.bvh_rmax = bv.rmax; p.bvh_mag = bv.mag;
         p.bvh_inv_rmin = env_u64("RT_AMD_LINEAR_E", 0) ? INFINITY : bv.inv_rmin;
+        // sphere-only scenes: primary rays test their pixel's candidates
+        if (d->ntri == 0 && env_u64("RT_AMD_SPHERE_LISTS", 1) != 0) {
+            prepare_primary_sphere_lists(w, cam, width, height);
+            if (d->spl_version != w.spl_version) {
+                if (d->spl) HIP_TRY(hipFree(d->spl));
+                d->spl = nullptr;
+                if (!w.spl.rec.empty()) {
+                    HIP_TRY(hipMalloc((void **)&d->spl, w.spl.rec.size() * 4));
+                    HIP_TRY(hipMemcpy(d->spl, w.spl.rec.data(), w.spl.rec.size() * 4,
+                                      hipMemcpyHostToDevice));
+                }
+                d->spl_version = w.spl_version;
+            }
+            p.spl = d->spl;
+        }
     }
     const bool use_tbvh = d->tnodes > 0 && o.accel != RT_ACCEL_BRUTE;
     if (use_tbvh) prepare_camera(w, cam);

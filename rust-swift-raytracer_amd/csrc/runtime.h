@@ -45,7 +45,9 @@ struct DeviceState {
     uint64_t cam_version = 0;                                  // WorldState::ctree_version uploaded
     uint32_t *ptl_off = nullptr, *ptl_items = nullptr;         // primary-ray triangle lists
     uint64_t ptl_version = 0;
-    size_t lds_bytes = 0;                                       // 0: tree not LDS-stageable
+    uint2 *spl = nullptr;                                       // primary sphere lists
+    uint64_t spl_version = 0;
+    size_t lds_bytes = 0;                                      // 0: tree not LDS-stageable
     float *samples = nullptr;        size_t samples_cap = 0;   // sample slab (3 planes)
     float *ring = nullptr;           size_t ring_cap = 0;      // per-wave sample rings (fused resolve)
     uint32_t *out = nullptr;         size_t out_cap = 0;       // RGBA8 tile (host path)
@@ -72,6 +74,10 @@ struct WorldState {
     CameraModel ptl_cam{};
     size_t ptl_w = 0, ptl_h = 0;
     uint64_t ptl_ctree = 0, ptl_version = 0;
+    PrimarySphereLists spl;       // for spl_cam at spl_w x spl_h
+    CameraModel spl_cam{};
+    size_t spl_w = 0, spl_h = 0;
+    uint64_t spl_version = 0;
     std::map<int, std::unique_ptr<DeviceState>> devices;
 };
 

@@ -257,7 +257,9 @@ def test_scheduling_knobs_do_not_change_samples(monkeypatch, scene):
                 dict(RT_AMD_STEP="1", RT_AMD_STEPS="5"), dict(RT_AMD_STEP="0"),
                 dict(RT_AMD_REFILL="17"), dict(RT_AMD_LDS="0"),
                 dict(RT_AMD_LDS="0", RT_AMD_STEP="1", RT_AMD_STEPS="3"),
-                dict(RT_AMD_LINEAR_E="1"), dict(RT_AMD_PRIMARY_LISTS="0")]:
+                dict(RT_AMD_LINEAR_E="1"), dict(RT_AMD_PRIMARY_LISTS="0"),
+                dict(RT_AMD_SPHERE_LISTS="0"), dict(RT_AMD_FUSED="0"),
+                dict(RT_AMD_RESOLVE_PIX="1"), dict(RT_AMD_RESOLVE_PIX="64")]:
         for k, v in env.items():
             monkeypatch.setenv(k, v)
         out, _ = render_kept(world, w, h, spp, 8)
@@ -348,6 +350,31 @@ def test_bvh_matches_oracle_rtow():
     assert_bits_equal(world.read_samples(64 * 36 * 4)[:, :3],
                       oracle_samples_to_gpu_order(smp, 64, 36, 4)[:, :3], "samples")
     assert gst["rays"] == st["rays"]
+
+
+def test_primary_sphere_lists_follow_camera_and_size(monkeypatch):
+    """Primary rays test per-pixel candidate lists built for the camera and
+    frame size (bvh.h PrimarySphereLists): after camera moves (one into the
+    sphere field, one far off, which falls back to the walk) and at several
+    sizes every sample equals the tree walk's and brute force."""
+    src = S.rtow()
+    world = R.World(src)
+    for mv, (w, h) in [((0.0, 0.0, 0.0), (96, 54)), ((0.0, 0.0, 0.0), (57, 31)),
+                       ((0.5, -1.5, -9.0), (80, 60)), ((3.0, 0.4, -14.0), (64, 36)),
+                       ((0.0, 0.0, 2000.0), (48, 27)), ((0.0, 0.0, -2000.0), (40, 30))]:
+        world.move_camera(*mv)
+        a, _ = render_kept(world, w, h, 4, 8, accel=R.ACCEL_BRUTE)
+        sa = world.read_samples(w * h * 4)
+        b, sb = render_kept(world, w, h, 4, 8, accel=R.ACCEL_BVH)
+        sb_ = world.read_samples(w * h * 4)
+        monkeypatch.setenv("RT_AMD_SPHERE_LISTS", "0")
+        c, sc = render_kept(world, w, h, 4, 8, accel=R.ACCEL_BVH)
+        sc_ = world.read_samples(w * h * 4)
+        monkeypatch.delenv("RT_AMD_SPHERE_LISTS")
+        assert_bits_equal(b, a, f"frame {mv} {w}x{h}")
+        assert_bits_equal(sb_[:, :3], sa[:, :3], f"samples (lists) {mv} {w}x{h}")
+        assert_bits_equal(sc_[:, :3], sa[:, :3], f"samples (walk) {mv} {w}x{h}")
+        assert sb["rays"] == sc["rays"]
 
 
 def test_bvh_full_size_c2_equals_brute_force():
