@@ -63,4 +63,24 @@ __device__ __forceinline__ float xdiv(float a, float b, float y) {
     return __builtin_fmaf(-r, y, q);
 }
 
+// RN(sqrt(a)) -- the bits of IEEE sqrtf (maths.rs:107 `f32::sqrt`,
+// common.rs:84) without the general expansion's denormal scaling and class
+// fix-up.  gfx950's v_sqrt_f32 is within one ulp of the exact root for every
+// positive normal input (tools/sqrt_probe.hip), so the correctly rounded root
+// is s, s - ulp or s + ulp; the two residuals a - s'*s (one fma each, exact
+// enough for a >= 2^-96) pick it, as in the general sequence.  Inputs below
+// 2^-96 (and zero, negatives, NaN) take HIP's sqrtf.  Checked on the device
+// against sqrtf for all 2^32 inputs (tools/exactdiv_check.hip).
+__device__ __forceinline__ float xsqrt(float a) {
+    const float s = __builtin_amdgcn_sqrtf(a);
+    const float sm = __uint_as_float(__float_as_uint(s) - 1u);
+    const float sp = __uint_as_float(__float_as_uint(s) + 1u);
+    const float rm = __builtin_fmaf(-sm, s, a);
+    const float rp = __builtin_fmaf(-sp, s, a);
+    float r = rm <= 0.0f ? sm : s;
+    r = rp > 0.0f ? sp : r;
+    if (__builtin_expect(!(a >= 0x1p-96f), 0)) r = __builtin_sqrtf(a);
+    return r;
+}
+
 }  // namespace rtamd

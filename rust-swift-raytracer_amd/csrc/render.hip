@@ -63,7 +63,7 @@ __device__ __forceinline__ F3 divide_by(F3 a, float b) {
     return F3{a.x / b, a.y / b, a.z / b};
 }
 __device__ __forceinline__ F3 unit(F3 a) {  // NVec3::new, maths.rs:111-118
-    const float len = __builtin_sqrtf((a.x * a.x + a.y * a.y) + a.z * a.z);
+    const float len = xsqrt((a.x * a.x + a.y * a.y) + a.z * a.z);
     return divide_by(a, len);
 }
 
@@ -146,7 +146,7 @@ __device__ __forceinline__ void spheres_brute(const TraceParams &p, F3 org, F3 d
 #pragma unroll
         for (uint32_t k = 0; k < kBatch; ++k) {
             if (disc[k] >= 0.0f) {
-                const float sq = __builtin_sqrtf(disc[k]);
+                const float sq = xsqrt(disc[k]);
                 const float r1 = -hb[k] - sq;
                 const float r2 = -hb[k] + sq;
                 const bool ok1 = (tmin < r1) && (r1 < best_t);
@@ -171,7 +171,7 @@ __device__ __forceinline__ bool sphere_candidate(float4 S, F3 org, F3 dir, int i
     const float cc = ((ocx * ocx + ocy * ocy) + ocz * ocz) - S.w;
     const float disc = hb * hb - cc;
     if (!(disc >= 0.0f)) return false;
-    const float sq = __builtin_sqrtf(disc);
+    const float sq = xsqrt(disc);
     const float r1 = -hb - sq;
     const float r2 = -hb + sq;
     const bool v1 = tmin < r1;
@@ -214,7 +214,7 @@ __device__ __forceinline__ float slab_rcp(float d) {
 struct SphBound { float A, e_abs; };  // per-ray inputs of the inflation
 __device__ __forceinline__ SphBound sph_bound(const TraceParams &p, F3 org) {
     const float ax = org.x - p.bvh_c[0], ay = org.y - p.bvh_c[1], az = org.z - p.bvh_c[2];
-    return SphBound{__builtin_sqrtf((ax * ax + ay * ay) + az * az) * 1.00001f + p.bvh_r,
+    return SphBound{xsqrt((ax * ax + ay * ay) + az * az) * 1.00001f + p.bvh_r,
                     2e-6f * ((fabsf(org.x) + fabsf(org.y)) + fabsf(org.z) + p.bvh_mag)};
 }
 constexpr float kErrKq = 40.5f * 0x1p-24f;  // 2.7 x 15u
@@ -827,7 +827,7 @@ __attribute__((amdgpu_waves_per_eu(RT_WAVES_PER_EU, 8))) void trace_kernel(Trace
                         if (dot(dir, nrm) >= 0.0f) { n2 = -nrm; eta = 1.0f / param; }
                         const float cos_t = dot(-dir, n2);  // maths.rs:31-36
                         const F3 perp = scale(dir + scale(n2, cos_t), eta);
-                        const F3 par = scale(n2, -__builtin_sqrtf(fabsf(1.0f - dot(perp, perp))));
+                        const F3 par = scale(n2, -xsqrt(fabsf(1.0f - dot(perp, perp))));
                         v = perp + par;
                         cr = cg = cb = 1.0f;
                     } else {  // Emission (materials.rs:100-102)

@@ -6,6 +6,7 @@
 //      the guarded range, random numerator exponents and signs).
 //   3. Numerator edge values (+-0, +-2^-60, +-(2^60 - ulp)) against every
 //      denominator of (2); the guard predicates on boundary values.
+//   4. xsqrt(a) == sqrtf(a) for all 2^32 inputs.
 // Prints the mismatch counts and exits 1 on any mismatch.
 // Build: hipcc --offload-arch=gfx950 -O3 -ffp-contract=off -I../rust-swift-raytracer_amd/csrc
 #include <hip/hip_runtime.h>
@@ -94,6 +95,16 @@ __global__ void edge_kernel(const uint32_t *den, uint32_t nden, Bad *bad, Bad *g
     }
 }
 
+// xsqrt(a) == sqrtf(a), bit for bit, for every 32-bit input (NaNs included)
+__global__ void sqrt_kernel(Bad *bad) {
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < (1ull << 32);
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t bits = (uint32_t)i;
+        const float a = __uint_as_float(bits);
+        if (__float_as_uint(xsqrt(a)) != __float_as_uint(__builtin_sqrtf(a))) record(bad, bits, 0);
+    }
+}
+
 static uint32_t xs32(uint32_t &s) {
     s ^= s << 13;
     s ^= s >> 17;
@@ -151,7 +162,16 @@ int main(int argc, char **argv) {
     printf("edges: %llu division mismatches, %llu guard errors", bad[1].count, bad[2].count);
     if (bad[2].count) printf(" (first value 0x%08x, case %u)", bad[2].first_a, bad[2].first_b);
     printf("\n");
-    const bool ok = bad[0].count == 0 && bad[1].count == 0 && bad[2].count == 0;
+    // 4. every square root
+    Bad *sq;
+    CHECK(hipMallocManaged(&sq, sizeof(Bad)));
+    *sq = Bad{0, 0, 0};
+    hipLaunchKernelGGL(sqrt_kernel, dim3(16384), dim3(256), 0, 0, sq);
+    CHECK(hipDeviceSynchronize());
+    printf("sqrt: all 2^32 inputs, %llu mismatches", sq->count);
+    if (sq->count) printf(" (first a=0x%08x)", sq->first_a);
+    printf("\n");
+    const bool ok = bad[0].count == 0 && bad[1].count == 0 && bad[2].count == 0 && sq->count == 0;
     printf("%s\n", ok ? "exactdiv OK" : "exactdiv FAILED");
     return ok ? 0 : 1;
 }
