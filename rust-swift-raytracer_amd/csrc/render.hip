@@ -113,6 +113,15 @@ __device__ __forceinline__ float4 uniform_load(const float4 *base, uint32_t i) {
 #endif
 }
 
+__device__ __forceinline__ uint32_t uniform_load_u32(const uint32_t *base, uint32_t i) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    typedef const __attribute__((address_space(4))) uint32_t *cu32_ptr;
+    return ((cu32_ptr)(const void *)base)[i];
+#else
+    return base[i];
+#endif
+}
+
 __device__ __forceinline__ uint32_t fdiv(uint32_t n, const FastDiv &f) { return fastdiv_apply(n, f); }
 
 constexpr uint32_t kWave = 64;
@@ -227,8 +236,10 @@ __device__ __forceinline__ float sph_inflation(const TraceParams &p, SphBound b,
 __device__ __forceinline__ void spheres_big(const TraceParams &p, F3 org, F3 dir, float &best_t,
                                             int &best_i) {
     for (uint32_t k = 0; k < p.nbig; ++k) {
+        // (both scalar loads: a vector load here made the ray setup wait on
+        // every outstanding vector memory op, vmcnt(0))
         const float4 S = uniform_load(p.big_hot, k);
-        sphere_candidate(S, org, dir, (int)p.big_id[k], best_t, best_i);
+        sphere_candidate(S, org, dir, (int)uniform_load_u32(p.big_id, k), best_t, best_i);
     }
 }
 
@@ -940,12 +951,6 @@ __attribute__((amdgpu_waves_per_eu(RT_WAVES_PER_EU, 8))) void trace_kernel(Trace
                 uint32_t s, col, row;
                 job_pixel(p, job, s, col, row);
                 slot = job + cur_off;
-                if (kBvh && !kMesh && p.spl != nullptr) {
-                    // loaded now, used at the ray's setup (next iteration)
-                    const uint2 r = p.spl[(size_t)(p.height - 1u - row) * p.width + col];
-                    spl0 = r.x;
-                    spl1 = r.y;
-                }
                 const uint64_t gjob = ((uint64_t)row * p.width + col) * p.spp + s;
                 rng = (p.mode == kRngReplay) ? p.replay[gjob] : counter_seed(p.seed, gjob);
                 // common.rs:335-337: u drawn before v; camera.rs:84-89
@@ -966,6 +971,13 @@ __attribute__((amdgpu_waves_per_eu(RT_WAVES_PER_EU, 8))) void trace_kernel(Trace
                 const F3 llc = f3(p.cam[3], p.cam[4], p.cam[5]);
                 vdir = ((llc + scale(h, u)) + scale(vv, v)) - org;  // normalised below
                 renorm = true;
+                if (kBvh && !kMesh && p.spl != nullptr) {
+                    // issued after the seed's (replay) load, so nothing waits on it
+                    // before the ray's setup in the next iteration
+                    const uint2 r = p.spl[(size_t)(p.height - 1u - row) * p.width + col];
+                    spl0 = r.x;
+                    spl1 = r.y;
+                }
                 thr_r = thr_g = thr_b = 1.0f;
                 bounce = 0;
                 phase = kSetup;
