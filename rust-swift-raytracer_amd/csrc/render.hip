@@ -509,47 +509,83 @@ __device__ __forceinline__ void tri_primary_list(const TraceParams &p, uint32_t 
         tri_record(p.cam_tris + 4u * p.ptl_items[j], org, dir, best_t, tri_t, tri_i, tri_in);
 }
 
-// Fused resolve of one finished chunk (wave-uniform call): jobs [base, base +
-// len) are whole pixels (chunks and partitions are pixel-aligned), their
-// samples sit at ring offset `off` of the wave's ring (planes `plane` floats
-// apart).  A lane per pixel sums the samples in order (common.rs:333-341,
-// the same fold as resolve_kernel), then gamma + `as u8` (:344-356).  The
-// samples were stored by this wave: a workgroup-scope fence orders them
-// (one CU, one L1).
+// One resolved pixel: gamma + `as u8` (common.rs:344-356), RGBA8 at the
+// tile row of launch-local pixel lp.
+__device__ __forceinline__ void resolve_store(const TraceParams &p, uint32_t lp, float r, float g,
+                                              float b) {
+    const uint32_t R = sat_u8(__builtin_sqrtf(r * p.inv_spp) * 255.999f);
+    const uint32_t G = sat_u8(__builtin_sqrtf(g * p.inv_spp) * 255.999f);
+    const uint32_t B = sat_u8(__builtin_sqrtf(b * p.inv_spp) * 255.999f);
+    const uint32_t q = fdiv(lp, p.div_width);
+    const uint32_t col = lp - q * p.width;
+    p.out[(size_t)(p.slab_row0 + q) * p.width + col] = R | (G << 8) | (B << 16) | (p.alpha_u8 << 24);
+}
+
+// Fused resolve of one finished chunk (wave-uniform call, all lanes active):
+// jobs [base, base + len) are whole pixels (chunks and partitions are
+// pixel-aligned), their samples sit at ring offset `off` of the wave's ring
+// (planes `plane` floats apart).  Each pixel's samples are summed in order
+// (common.rs:333-341, the same fold as resolve_kernel).  The samples were
+// stored by this wave: a workgroup-scope fence orders them (one CU, one L1).
+//
+// L lanes per pixel (a power of two, L * pixels <= 64): per round, lane j of
+// pixel g's group loads samples 4j .. 4j+3 of the round's 4L (one float4 per
+// plane, all loads of the round in flight together), then every lane of the
+// group folds the group's 4L values in sample order through ds_bpermute, so
+// the fold's latency is one load round trip per round instead of one per
+// float4.  Chunks whose spp does not split this way, and the triangle
+// kernels (kGroup false: at the VGPR cap the group fold adds scratch; C5
+// +0.7 %), sum one pixel per lane (C2: -0.6 % for the group fold).
+template <bool kGroup>
 __device__ __forceinline__ void resolve_chunk(const TraceParams &p, const float *ring, uint32_t plane,
-                                           uint32_t off, uint32_t base, uint32_t len,
-                                           uint32_t lane) {
+                                              uint32_t off, uint32_t base, uint32_t len,
+                                              uint32_t lane) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
     const uint32_t spp = p.spp;
     const uint32_t np = fdiv(len, p.div_spp), pix0 = fdiv(base, p.div_spp);
+    uint32_t sh = 0;  // L = 2^sh: 4L | spp, L * np <= 64
+    while ((2u << sh) * np <= kWave && spp % (8u << sh) == 0) ++sh;
+    if (kGroup && sh > 0 && (spp & 3u) == 0) {
+        const uint32_t L = 1u << sh, step = 4u * L;
+        const uint32_t g = lane >> sh, j = lane & (L - 1u);
+        const bool on = g < np;
+        const float *src = ring + off + (on ? g * spp : 0u) + 4u * j;
+        const float4 z = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        auto ld = [&](uint32_t k, float4 &R, float4 &G, float4 &B) {
+            R = G = B = z;
+            if (on) {
+                R = *reinterpret_cast<const float4 *>(src + k);
+                G = *reinterpret_cast<const float4 *>(src + plane + k);
+                B = *reinterpret_cast<const float4 *>(src + 2 * plane + k);
+            }
+        };
+        float ar = 0.0f, ag = 0.0f, ab = 0.0f;
+        for (uint32_t k = 0; k < spp; k += step) {
+            float4 R, G, B;
+            ld(k, R, G, B);
+            for (uint32_t t = 0; t < L; ++t) {
+                const int sl = (int)((g << sh) + t);
+                ar = ar + __shfl(R.x, sl); ar = ar + __shfl(R.y, sl);
+                ar = ar + __shfl(R.z, sl); ar = ar + __shfl(R.w, sl);
+                ag = ag + __shfl(G.x, sl); ag = ag + __shfl(G.y, sl);
+                ag = ag + __shfl(G.z, sl); ag = ag + __shfl(G.w, sl);
+                ab = ab + __shfl(B.x, sl); ab = ab + __shfl(B.y, sl);
+                ab = ab + __shfl(B.z, sl); ab = ab + __shfl(B.w, sl);
+            }
+        }
+        if (on && j == 0) resolve_store(p, pix0 + g, ar, ag, ab);
+        return;
+    }
     for (uint32_t i = lane; i < np; i += kWave) {
         const float *src = ring + off + i * spp;
         float r = 0.0f, g = 0.0f, b = 0.0f;
-        if ((spp & 3u) == 0) {
-            // (no unrolling: #pragma unroll 4 here spilled the whole kernel)
-            for (uint32_t k = 0; k < spp; k += 4) {
-                const float4 R = *reinterpret_cast<const float4 *>(src + k);
-                const float4 G = *reinterpret_cast<const float4 *>(src + plane + k);
-                const float4 B = *reinterpret_cast<const float4 *>(src + 2 * plane + k);
-                r = r + R.x; r = r + R.y; r = r + R.z; r = r + R.w;
-                g = g + G.x; g = g + G.y; g = g + G.z; g = g + G.w;
-                b = b + B.x; b = b + B.y; b = b + B.z; b = b + B.w;
-            }
-        } else {
-            for (uint32_t k = 0; k < spp; ++k) {
-                r = r + src[k];
-                g = g + src[plane + k];
-                b = b + src[2 * plane + k];
-            }
+        for (uint32_t k = 0; k < spp; ++k) {
+            r = r + src[k];
+            g = g + src[plane + k];
+            b = b + src[2 * plane + k];
         }
-        const uint32_t R = sat_u8(__builtin_sqrtf(r * p.inv_spp) * 255.999f);
-        const uint32_t G = sat_u8(__builtin_sqrtf(g * p.inv_spp) * 255.999f);
-        const uint32_t B = sat_u8(__builtin_sqrtf(b * p.inv_spp) * 255.999f);
-        const uint32_t lp = pix0 + i;
-        const uint32_t q = fdiv(lp, p.div_width);
-        const uint32_t col = lp - q * p.width;
-        p.out[(size_t)(p.slab_row0 + q) * p.width + col] = R | (G << 8) | (B << 16) | (p.alpha_u8 << 24);
+        resolve_store(p, pix0 + i, r, g, b);
     }
 }
 
@@ -892,7 +928,8 @@ __attribute__((amdgpu_waves_per_eu(RT_WAVES_PER_EU, 8))) void trace_kernel(Trace
                     rleft[k] -= n;
                     if (n != 0 && rleft[k] == 0) {
                         if (!(p.ablate & 2u))
-                            resolve_chunk(p, sbase, pstride, k << p.ring_shift, rbase[k], rlen[k], lane);
+                            resolve_chunk<!kMesh>(p, sbase, pstride, k << p.ring_shift, rbase[k],
+                                                  rlen[k], lane);
                         rfree |= 1u << k;
                     }
                 }
@@ -974,9 +1011,14 @@ __attribute__((amdgpu_waves_per_eu(RT_WAVES_PER_EU, 8))) void trace_kernel(Trace
                 if (kBvh && !kMesh && p.spl != nullptr) {
                     // issued after the seed's (replay) load, so nothing waits on it
                     // before the ray's setup in the next iteration
-                    const uint2 r = p.spl[(size_t)(p.height - 1u - row) * p.width + col];
-                    spl0 = r.x;
-                    spl1 = r.y;
+                    if (p.ablate & 4u) {  // timing-only diagnostic: no record load
+                        spl0 = 0;
+                        spl1 = 0;
+                    } else {
+                        const uint2 r = p.spl[(size_t)(p.height - 1u - row) * p.width + col];
+                        spl0 = r.x;
+                        spl1 = r.y;
+                    }
                 }
                 thr_r = thr_g = thr_b = 1.0f;
                 bounce = 0;
