@@ -13,6 +13,7 @@ enum : uint32_t { kRngCounter = 1, kRngReplay = 2 };
 enum : uint32_t { kMatDiffuse = 0, kMatMetal = 1, kMatDielectric = 2, kMatEmission = 3 };
 constexpr uint32_t kPrimaryTriStripW = 8;  // bvh.h kTriStripW
 constexpr uint32_t kTraceRing = 4;         // chunk slots per wave (fused resolve)
+constexpr uint32_t kStatSlots = 16;        // u64 counters per wave record (TraceParams::stats)
 
 // Kernel argument block (lives in the kernarg segment -> SGPRs).
 struct TraceParams {
@@ -33,8 +34,10 @@ struct TraceParams {
     float inv_spp;            // 1.0 / spp as f32 (common.rs:345)
     uint32_t alpha_u8;        // the alpha byte: every pixel's is the same (resolve_kernel)
     uint32_t *job_counter;    // nparts counters, 32 u32 apart; zeroed before every launch
-    unsigned long long *stats;// rays, tri in t-range, BVH sphere tests, BVH node tests,
-                              // 4 stamp counters, triangle-BVH node tests
+    unsigned long long *stats;// nullptr, or kStatSlots per wave (wave = block * waves per
+                              // block + wave in block): rays, tri in t-range, BVH sphere
+                              // tests, BVH node tests, 4 stamp counters, triangle-BVH node
+                              // tests, triangle tests
     const uint32_t *replay;   // REPLAY start states (global job index)
     float cam[12];            // origin, lower_left, horizontal, vertical
     float wden, hden;         // (width-1) as f32, (height-1) as f32

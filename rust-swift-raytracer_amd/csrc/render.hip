@@ -1038,19 +1038,22 @@ __attribute__((amdgpu_waves_per_eu(RT_WAVES_PER_EU, 8))) void trace_kernel(Trace
         if (__ballot(active) == 0 && exhausted) break;
     }
 
-    // ---- per-wave statistics: one atomic per counter per wave ------------
-#ifdef RT_STAMPS
-    if (lane == 0)
-        for (int k = 0; k < 4; ++k) atomicAdd(&p.stats[4 + k], (unsigned long long)stamp_acc[k]);
-#endif
+    // ---- per-wave statistics (stats requested only): each wave adds its
+    // counters to its own 16-slot record, no atomics -- 6144 waves' atomics on
+    // the same six words serialised at the end of every launch (~0.4 ms, most
+    // of a multi-GPU tile's overhead); the host sums the records
+    if (p.stats == nullptr) return;
     uint64_t c[6] = {rays, tri_in, sph_tests, node_tests, tnode_tests, tri_done};
 #pragma unroll
     for (int k = 0; k < 6; ++k)
         for (uint32_t off = kWave / 2; off > 0; off >>= 1) c[k] += __shfl_xor(c[k], (int)off);
     if (lane == 0) {
+        unsigned long long *w = p.stats + (size_t)wave_id * kStatSlots;
 #pragma unroll
-        for (int k = 0; k < 6; ++k)
-            if (c[k]) atomicAdd(&p.stats[k < 4 ? k : k + 4], (unsigned long long)c[k]);
+        for (int k = 0; k < 6; ++k) w[k < 4 ? k : k + 4] += c[k];
+#ifdef RT_STAMPS
+        for (int k = 0; k < 4; ++k) w[4 + k] += stamp_acc[k];
+#endif
     }
 }
 

@@ -175,7 +175,6 @@ static int device_for(WorldState &w, int want, DeviceState *&out) {
             d->blocks_per_cu_bvh[st] = std::max(d->blocks_per_cu_bvh[st], 1);
         }
         HIP_TRY(hipMalloc((void **)&d->counter, kMaxParts * 128));
-        HIP_TRY(hipMalloc((void **)&d->stats, 128));
         slot = std::move(d);
     }
     out = slot.get();
@@ -273,7 +272,6 @@ int render_frame(WorldState &w, const CameraModel &cam, size_t width, size_t hei
         HIP_TRY(grow(d->replay, d->replay_cap, n));
         HIP_TRY(hipMemcpyAsync(d->replay, o.replay_states, n * 4, hipMemcpyHostToDevice, s));
     }
-    HIP_TRY(hipMemsetAsync(d->stats, 0, 128, s));
 
     TraceParams p{};
     p.sph_hot = d->sph_hot; p.sph_cold = d->sph_cold;
@@ -281,7 +279,6 @@ int render_frame(WorldState &w, const CameraModel &cam, size_t width, size_t hei
     p.mats = d->mats;
     p.samples = d->samples;
     p.job_counter = d->counter;
-    p.stats = d->stats;
     p.replay = d->replay;
     const Vec3 cv[4] = {cam.origin, cam.lower_left, cam.horizontal, cam.vertical};
     for (int i = 0; i < 4; ++i) { p.cam[3 * i] = cv[i].x; p.cam[3 * i + 1] = cv[i].y; p.cam[3 * i + 2] = cv[i].z; }
@@ -424,6 +421,14 @@ int render_frame(WorldState &w, const CameraModel &cam, size_t width, size_t hei
     double trace_ms = 0.0, resolve_ms = 0.0;
     uint32_t launches = 0, waves = 0;
     const bool timed = stats != nullptr;  // HIP-event timing + counters need a host wait
+    // counters only when asked for: one 16-slot record per wave, summed here
+    const uint64_t max_waves = full_blocks * waves_per_block;
+    p.stats = nullptr;
+    if (timed) {
+        HIP_TRY(grow(d->stats, d->stats_cap, max_waves * kStatSlots));
+        HIP_TRY(hipMemsetAsync(d->stats, 0, max_waves * kStatSlots * 8, s));
+        p.stats = d->stats;
+    }
     for (size_t r0 = 0; r0 < T; r0 += rows_per_slab) {
         const size_t rows = std::min(rows_per_slab, T - r0);
         const uint64_t njobs = rows * jobs_per_row;
@@ -447,8 +452,12 @@ int render_frame(WorldState &w, const CameraModel &cam, size_t width, size_t hei
                 // A/B, C2: 4 px 7.10 ms, 8 px 6.79, 16 px 6.83, 32 px 7.36,
                 // slab + resolve_kernel 6.94).  Sliced walks keep their chunk
                 // (C5: 16 px +1.5 %, 4 px = slab)
-                const uint64_t px = std::max<uint64_t>(1, std::min<uint64_t>(
+                uint64_t px = std::max<uint64_t>(1, std::min<uint64_t>(
                     env_u64("RT_AMD_RESOLVE_PIX", p.step ? 1 : 8), 4096 / spp));
+                // small launches (multi-GPU tiles) keep >= 16 chunks per wave
+                // where 4-pixel chunks allow it (C2 tile of 8 ranks: 8 px 1.12 ms,
+                // 4 px 1.04, 2 px 1.22)
+                while (px > 4 && njobs / (nwaves * px * spp) < 16) px /= 2;
                 chunk = std::max<uint64_t>(chunk, px * spp);
             }
             p.chunk = (uint32_t)chunk;
@@ -487,9 +496,11 @@ int render_frame(WorldState &w, const CameraModel &cam, size_t width, size_t hei
     }
     // without stats the frame stays asynchronous on the stream (no host wait)
     if (!timed) return 0;
-    unsigned long long st[16] = {};
-    HIP_TRY(hipMemcpyAsync(st, d->stats, 128, hipMemcpyDeviceToHost, s));
+    std::vector<unsigned long long> rec(max_waves * kStatSlots);
+    HIP_TRY(hipMemcpyAsync(rec.data(), d->stats, rec.size() * 8, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
+    unsigned long long st[kStatSlots] = {};
+    for (size_t i = 0; i < rec.size(); ++i) st[i % kStatSlots] += rec[i];
     if (stats) {
         stats->samples = (uint64_t)T * jobs_per_row;
         stats->rays = st[0];

@@ -53,7 +53,7 @@ struct DeviceState {
     uint32_t *out = nullptr;         size_t out_cap = 0;       // RGBA8 tile (host path)
     uint32_t *replay = nullptr;      size_t replay_cap = 0;
     uint32_t *counter = nullptr;                                // job counter
-    unsigned long long *stats = nullptr;                        // TraceParams::stats (16 slots)
+    unsigned long long *stats = nullptr; size_t stats_cap = 0;  // per-wave counter records
     // resident workgroups per CU of each kernel variant, [0]: whole walks, [1]: sliced walks
     int blocks_per_cu[2] = {0, 0}, blocks_per_cu_bvh[2] = {0, 0}, blocks_per_cu_lds[2] = {0, 0};
     int num_cus = 0;
