@@ -2,7 +2,9 @@
 compiled with g++ against csrc/bvh.cpp + csrc/scene.cpp.  Every primitive in
 exactly one leaf, nested boxes (and nested normal boxes), octant links that
 walk every node once, quantised kernel nodes that decode to conservative
-boxes and round-trip their child/leaf words (bvh.h)."""
+boxes and round-trip their child/leaf words (bvh.h).  tests/sphere_list_check.cpp:
+every tree sphere that yields a candidate for a primary ray (reference f32
+arithmetic) is in that pixel's primary sphere list (bvh.h PrimarySphereLists)."""
 import os
 import subprocess
 
@@ -50,3 +52,26 @@ def test_triangle_trees(checker, tmp_path, case, leaf):
 def test_mesh_c5_trees(checker, tmp_path):
     out = run(checker, tmp_path, S.mesh(nx=100, ny=80))
     assert "triangles 16000 tree 16000" in out
+
+
+@pytest.fixture(scope="module")
+def list_checker(tmp_path_factory):
+    exe = str(tmp_path_factory.mktemp("spl") / "sphere_list_check")
+    subprocess.run(["g++", "-O2", "-std=c++17", "-ffp-contract=off", f"-I{CSRC}",
+                    os.path.join(ROOT, "tests", "sphere_list_check.cpp"), os.path.join(CSRC, "bvh.cpp"),
+                    os.path.join(CSRC, "scene.cpp"), "-o", exe], check=True)
+    return exe
+
+
+@pytest.mark.parametrize("w,h,move", [
+    (160, 90, None), (97, 61, None), (64, 36, (0.5, -1.5, -9.0)), (80, 45, (3.0, 0.4, -14.0)),
+    (120, 68, (-6.0, 3.0, 4.0)), (2, 2, None),
+])
+def test_primary_sphere_lists_cover_every_candidate(list_checker, tmp_path, w, h, move):
+    path = tmp_path / "rtow.txt"
+    path.write_text(S.rtow())
+    args = [list_checker, str(path), str(w), str(h)] + ([str(x) for x in move] if move else [])
+    r = subprocess.run(args, capture_output=True, text=True)
+    assert r.returncode == 0 and "OK" in r.stdout, r.stdout + r.stderr
+    if move is None and w > 2:
+        assert "candidates 0" not in r.stdout  # the frame does see tree spheres
