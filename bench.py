@@ -128,14 +128,23 @@ def main():
     dev = torch.device("cuda", local_rank)
     tile = torch.zeros(max_rows * W * 4, dtype=torch.uint8, device=dev)
     gathered = torch.empty(nr * max_rows * W * 4, dtype=torch.uint8, device=dev) if nr > 1 else None
-    stream = torch.cuda.current_stream(dev)
+    # one explicit stream for the frames, their HIP events and the RCCL
+    # gather (the default stream's handle is 0, which the library would
+    # replace with its own stream)
+    stream = torch.cuda.Stream(device=dev)
+    torch.cuda.set_stream(stream)
 
-    def step(with_stats):
-        # timed steps run without counters: the frame is only enqueued (no host
-        # wait), so frames and the RCCL gather pipeline on the stream
+    def step(with_stats, ev=None):
+        # timed steps run without counters (the kernel variant whose work
+        # counters compile away): the frame is only enqueued (no host wait), so
+        # frames and the RCCL gather pipeline on the stream
+        if ev is not None:
+            ev[0].record(stream)
         st = world.render_device(W, H, tile.data_ptr(), stream.cuda_stream, spp=spp, depth=depth,
                                  row_block=ROW_BLOCK, rank=rank, nranks=nr, device=local_rank,
                                  accel=accel, stats=with_stats)
+        if ev is not None:
+            ev[1].record(stream)
         if nr > 1:
             if backend == "nccl":
                 tiles.gather(tile, gathered)  # RCCL all-gather over xGMI
@@ -149,20 +158,27 @@ def main():
     torch.cuda.synchronize()
     if nr > 1:
         dist.barrier()
+    # HIP events (torch's current stream is the launch stream) around each
+    # timed frame's render: the trace kernel's launch duration for the roofline
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+           for _ in range(args.steps)]
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step(False)
+    for k in range(args.steps):
+        step(False, evs[k])
     torch.cuda.synchronize()
     if nr > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    # kernel timing for the roofline: HIP events around the trace launches of
-    # frames like the timed ones, on the same stream, right after the timed region
+    # work counters of frames like the timed ones (the counting kernel variant),
+    # right after the timed region
     stats = [step(True) for _ in range(max(1, min(args.steps, 3)))]
     assert all(s["rays"] == st_warm["rays"] for s in stats), "frames must be identical"
 
     rays = st_warm["rays"] * args.steps
-    trace_ms = sum(s["trace_ms"] for s in stats) / max(1, sum(s["trace_launches"] for s in stats))
+    # (a timed frame is one job-counter fill + the trace launches)
+    trace_ms = (sum(a.elapsed_time(b) for a, b in evs) / args.steps
+                / max(1, stats[-1]["trace_launches"]))
+    count_trace_ms = sum(s["trace_ms"] for s in stats) / max(1, sum(s["trace_launches"] for s in stats))
     if nr > 1:
         tdev = dev if backend == "nccl" else torch.device("cpu")
         t_max = torch.tensor([elapsed], dtype=torch.float64, device=tdev)
@@ -216,6 +232,7 @@ def main():
                      "peak": FP32_VECTOR_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": achieved_tflops / FP32_VECTOR_PEAK_TFLOPS, "traffic": traffic,
                      "kernel": "trace_kernel", "avg_launch_ms": trace_ms,
+                     "counting_variant_ms": count_trace_ms,
                      "flops_per_launch": flops_per_launch, "flops": "executed work",
                      "brute_force_equivalent_tflops": alg_tflops,
                      "algorithmic_hbm_gbs": out_bytes / (trace_ms * 1e-3) / 1e9,

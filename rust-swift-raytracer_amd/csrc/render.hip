@@ -610,7 +610,7 @@ __device__ __forceinline__ void resolve_chunk(const TraceParams &p, const float 
 #endif
 // kMesh: the scene has triangles (else the whole Mesh::hit stage compiles
 // away, which keeps the sphere-only kernel's register allocation small).
-template <bool kBvh, bool kLds, bool kStep, bool kMesh>
+template <bool kBvh, bool kLds, bool kStep, bool kMesh, bool kCount>
 __global__ __launch_bounds__(kLds ? (kMesh ? 512 : RT_LDS_BLOCK_SPHERES) : 256)
 __attribute__((amdgpu_waves_per_eu(RT_WAVES_PER_EU, 8))) void trace_kernel(TraceParams p) {
     const uint32_t lane = __lane_id();
@@ -1042,7 +1042,7 @@ __attribute__((amdgpu_waves_per_eu(RT_WAVES_PER_EU, 8))) void trace_kernel(Trace
     // counters to its own 16-slot record, no atomics -- 6144 waves' atomics on
     // the same six words serialised at the end of every launch (~0.4 ms, most
     // of a multi-GPU tile's overhead); the host sums the records
-    if (p.stats == nullptr) return;
+    if (!kCount || p.stats == nullptr) return;  // (!kCount: the counters compile away)
     uint64_t c[6] = {rays, tri_in, sph_tests, node_tests, tnode_tests, tri_done};
 #pragma unroll
     for (int k = 0; k < 6; ++k)
@@ -1134,29 +1134,37 @@ size_t trace_lds_bytes(const TraceParams &p) {
     return (size_t)p.nnodes * 48 + (size_t)p.nprims * 20 + (size_t)p.nsph_padded * 36;
 }
 
-template <bool kStep, bool kMesh>
+template <bool kStep, bool kMesh, bool kCount>
 static void launch_trace_t(const TraceParams &p, uint32_t blocks, hipStream_t stream) {
     if (p.nnodes && p.use_lds)
-        hipLaunchKernelGGL((trace_kernel<true, true, kStep, kMesh>), dim3(blocks),
+        hipLaunchKernelGGL((trace_kernel<true, true, kStep, kMesh, kCount>), dim3(blocks),
                            dim3(trace_block_threads(true, kMesh)),
                            trace_lds_bytes(p), stream, p);
     else if (p.nnodes)
-        hipLaunchKernelGGL((trace_kernel<true, false, kStep, kMesh>), dim3(blocks), dim3(256), 0, stream,
-                           p);
+        hipLaunchKernelGGL((trace_kernel<true, false, kStep, kMesh, kCount>), dim3(blocks), dim3(256), 0,
+                           stream, p);
     else
-        hipLaunchKernelGGL((trace_kernel<false, false, kStep, kMesh>), dim3(blocks), dim3(256), 0, stream,
-                           p);
+        hipLaunchKernelGGL((trace_kernel<false, false, kStep, kMesh, kCount>), dim3(blocks), dim3(256), 0,
+                           stream, p);
 }
 
-hipError_t launch_trace(const TraceParams &p, uint32_t blocks, hipStream_t stream) {
+template <bool kCount>
+static void launch_trace_c(const TraceParams &p, uint32_t blocks, hipStream_t stream) {
     const bool tri = p.ntri != 0;
     if (p.step) {
-        if (tri) launch_trace_t<true, true>(p, blocks, stream);
-        else launch_trace_t<true, false>(p, blocks, stream);
+        if (tri) launch_trace_t<true, true, kCount>(p, blocks, stream);
+        else launch_trace_t<true, false, kCount>(p, blocks, stream);
     } else {
-        if (tri) launch_trace_t<false, true>(p, blocks, stream);
-        else launch_trace_t<false, false>(p, blocks, stream);
+        if (tri) launch_trace_t<false, true, kCount>(p, blocks, stream);
+        else launch_trace_t<false, false, kCount>(p, blocks, stream);
     }
+}
+
+// Frames rendered without stats run a variant whose work counters compile away
+// (one VALU increment per node / sphere test / ray).
+hipError_t launch_trace(const TraceParams &p, uint32_t blocks, hipStream_t stream) {
+    if (p.stats) launch_trace_c<true>(p, blocks, stream);
+    else launch_trace_c<false>(p, blocks, stream);
     return hipGetLastError();
 }
 
@@ -1174,13 +1182,13 @@ template <bool kStep, bool kMesh>
 static hipError_t trace_occupancy_t(int *blocks_per_cu, int variant, size_t lds_bytes) {
     if (variant == 2)
         return hipOccupancyMaxActiveBlocksPerMultiprocessor(
-            blocks_per_cu, trace_kernel<true, true, kStep, kMesh>, trace_block_threads(true, kMesh),
+            blocks_per_cu, trace_kernel<true, true, kStep, kMesh, true>, trace_block_threads(true, kMesh),
             lds_bytes);
     if (variant == 1)
         return hipOccupancyMaxActiveBlocksPerMultiprocessor(
-            blocks_per_cu, trace_kernel<true, false, kStep, kMesh>, 256, 0);
+            blocks_per_cu, trace_kernel<true, false, kStep, kMesh, true>, 256, 0);
     return hipOccupancyMaxActiveBlocksPerMultiprocessor(
-        blocks_per_cu, trace_kernel<false, false, kStep, kMesh>, 256, 0);
+        blocks_per_cu, trace_kernel<false, false, kStep, kMesh, true>, 256, 0);
 }
 
 hipError_t trace_occupancy(int *blocks_per_cu, int variant, size_t lds_bytes, bool step, bool tri) {

@@ -231,21 +231,22 @@ class World:
 
     def render(self, width, height, spp=16, depth=8, mode=RNG_COUNTER, seed=DEFAULT_SEED,
                replay=None, row_block=1, rank=0, nranks=1, device=-1, accel=ACCEL_AUTO,
-               keep_samples=False):
+               keep_samples=False, stats=True):
         """rt_render_ex -> (rgba uint8[tile_rows, width, 4], stats dict).
         keep_samples: write every sample to the slab (for read_samples) and
-        resolve with the second kernel; the frame is bit-identical."""
+        resolve with the second kernel; the frame is bit-identical.
+        stats=False: no counters (the kernel variant without them; stats None)."""
         o, keep = options(spp, depth, mode, seed, replay, row_block, rank, nranks, device, accel,
                           keep_samples, self._L)
         rows = int(self._L.rt_tile_rows(height, row_block, rank, nranks)) if nranks > 1 else height
         px = np.zeros((rows, width, 4), np.uint8)
         fb = CFramebuffer(width, height, px.ctypes.data_as(C.POINTER(ColorU8)))
         st = RenderStats()
-        rc = self._L.rt_render_ex(fb, self._h, C.byref(o), C.byref(st))
+        rc = self._L.rt_render_ex(fb, self._h, C.byref(o), C.byref(st) if stats else None)
         del keep
         if rc != 0:
             raise RenderError(f"rt_render_ex failed ({rc}): {self._L.rt_last_error().decode()}")
-        return px, st.as_dict()
+        return px, (st.as_dict() if stats else None)
 
     def read_samples(self, njobs, device=-1):
         """Per-sample colours of the last trace launch: float32[njobs, 4]."""

@@ -42,12 +42,15 @@ def assert_bits_equal(a, b, what):
 
 
 def render_kept(world, *args, **kw):
-    """Renders twice: by default (pixels resolved inside the trace kernel from
-    per-wave sample rings) and with keep_samples (every sample to the slab,
-    then resolve_kernel).  Both frames must agree bit for bit; afterwards the
+    """Renders three times: by default (pixels resolved inside the trace kernel
+    from per-wave sample rings), with keep_samples (every sample to the slab,
+    then resolve_kernel), and without stats (the kernel variant whose work
+    counters compile away).  The frames must agree bit for bit; afterwards the
     samples are readable (world.read_samples)."""
     out, st = world.render(*args, **kw)
-    kept, st2 = world.render(*args, keep_samples=True, **kw)
+    lean, _ = world.render(*args, stats=False, **kw)  # the kernel without work counters
+    assert_bits_equal(lean, out, "kernel without counters")
+    kept, st2 = world.render(*args, keep_samples=True, **kw)  # last: leaves the slab readable
     assert_bits_equal(kept, out, "in-kernel resolve vs slab + resolve kernel")
     assert st2["rays"] == st["rays"]
     return out, st

@@ -54,7 +54,7 @@ def main():
                 os.environ.pop(k, None)
             else:
                 os.environ[k] = v
-    res = {label: {"trace": [], "frame": [], "rays": 0} for label, _, _ in variants}
+    res = {label: {"trace": [], "frame": [], "lean": [], "rays": 0} for label, _, _ in variants}
     for rnd in range(args.rounds + 1):
         for label, world, env in variants:
             saved = {k: os.environ.get(k) for k in env}
@@ -65,6 +65,13 @@ def main():
                                      depth=depth, device=0, accel=accel)
             torch.cuda.synchronize()
             dt = (time.perf_counter() - t) * 1e3
+            # frames without stats (the bench's timed path: counters compiled out)
+            t = time.perf_counter()
+            for _ in range(3):
+                world.render_device(W, H, out.data_ptr(), stream.cuda_stream, spp=spp, depth=depth,
+                                    device=0, accel=accel, stats=False)
+            torch.cuda.synchronize()
+            lean = (time.perf_counter() - t) * 1e3 / 3
             for k, v in saved.items():
                 if v is None:
                     os.environ.pop(k, None)
@@ -74,12 +81,14 @@ def main():
                 continue  # warm-up round
             res[label]["trace"].append(st["trace_ms"])
             res[label]["frame"].append(dt)
+            res[label]["lean"].append(lean)
             res[label]["rays"] = st["rays"]
     for label, r in res.items():
         print(json.dumps({"variant": label, "config": args.config, "spp": spp,
                           "trace_ms_median": statistics.median(r["trace"]),
                           "trace_ms_min": min(r["trace"]),
                           "frame_ms_median": statistics.median(r["frame"]),
+                          "lean_frame_ms_median": statistics.median(r["lean"]),
                           "grays_per_s": r["rays"] / statistics.median(r["frame"]) / 1e6,
                           "rays": r["rays"]}))
 

@@ -17,9 +17,14 @@ import sys
 
 
 def short(name):
-    for k in ("trace_kernel", "resolve_kernel"):
-        if k in name:
-            return k
+    # trace_kernel<kBvh, kLds, kStep, kMesh, kCount>: the timed frames run the
+    # kCount=false variant ("trace_kernel"); frames with stats run
+    # "trace_kernel[count]"
+    if "trace_kernel" in name:
+        args = name.split("trace_kernel<", 1)[-1].split(">", 1)[0].replace(" ", "").split(",")
+        return "trace_kernel[count]" if len(args) == 5 and args[4] == "true" else "trace_kernel"
+    if "resolve_kernel" in name:
+        return "resolve_kernel"
     return name[:60]
 
 
@@ -39,7 +44,7 @@ def main(src, dst, config="c2"):
         for r in csv.DictReader(open(f)):
             agg[(short(r["Kernel_Name"]), r["Counter_Name"])].append(float(r["Counter_Value"]))
         for (kern, ctr), v in agg.items():
-            if kern in ("trace_kernel", "resolve_kernel"):
+            if kern in ("trace_kernel", "trace_kernel[count]", "resolve_kernel"):
                 out["kernels"].setdefault(kern, {})[ctr] = sum(v) / len(v)
     for k in out["kernels"].values():
         if "FETCH_SIZE" in k and "WRITE_SIZE" in k:
