@@ -249,7 +249,7 @@ __device__ __forceinline__ void spheres_big(const TraceParams &p, F3 org, F3 dir
 // sphere_leaf.  (Deferring leaf tests until every lane of the wave has one
 // pending -- "while-while" -- measured 6% slower on C2 and 60% on C5.)
 template <bool kLds>
-__device__ __forceinline__ void sphere_node(const BvhView &v, F3 inv, uint32_t oct, float best_t,
+__device__ __forceinline__ bool sphere_node(const BvhView &v, F3 inv, uint32_t oct, float best_t,
                                             F3 nlo, F3 nhi, uint32_t &node, uint32_t &leaf,
                                             uint32_t &node_tests) {
     ++node_tests;
@@ -268,12 +268,21 @@ __device__ __forceinline__ void sphere_node(const BvhView &v, F3 inv, uint32_t o
     const float t0z = __builtin_fmaf(B0.z, inv.z, nlo.z), t1z = __builtin_fmaf(B1.z, inv.z, nhi.z);
     const float tn = fmaxf(fmaxf(fminf(t0x, t1x), fminf(t0y, t1y)), fminf(t0z, t1z));
     const float tf = fminf(fminf(fmaxf(t0x, t1x), fmaxf(t0y, t1y)), fmaxf(t0z, t1z));
-    const bool skip = tn > tf || tf < 0.001f || tn > best_t;
+    // tn > best_t as a signed-integer compare: best_t is positive (or +inf)
+    // and tn is finite for any ray that can produce a candidate (inv and the
+    // slab offsets are finite), so the orders agree; a NaN ray has no
+    // candidate, so skipping for it changes nothing.  (As a float compare the
+    // compiler folds it into tn > min(tf, best_t) and canonicalises best_t at
+    // every node.)
+    const bool skip = tn > tf || tf < 0.001f || __float_as_int(tn) > __float_as_int(best_t);
     const uint32_t a = __float_as_uint(B0.w);
     const bool is_leaf = (a & kLeafBitDev) != 0;
     const uint32_t child = a + ((oct >> __float_as_uint(B1.w)) & 1u);  // near child first
     node = (skip || is_leaf) ? miss : child;
-    if (!skip && is_leaf) leaf = ((a & ~kLeafBitDev) << 3) | __float_as_uint(B1.w);
+    // (returned as a flag, so the caller branches on it directly; leaf is only
+    // read when it is set)
+    leaf = ((a & ~kLeafBitDev) << 3) | __float_as_uint(B1.w);
+    return !skip && is_leaf;
 }
 
 // The walk's per-ray slab offsets for inflation e: nlo = -((o + e) inv),
@@ -777,9 +786,8 @@ __attribute__((amdgpu_waves_per_eu(RT_WAVES_PER_EU, 8))) void trace_kernel(Trace
                 F3 nlo, nhi;
                 sphere_slabs(org, inv, sph_inflation(p, bnd, best_t), nlo, nhi);
                 do {
-                    uint32_t leaf = 0;
-                    sphere_node<kLds>(view, inv, oct, best_t, nlo, nhi, node, leaf, node_tests);
-                    if (leaf != 0)
+                    uint32_t leaf;
+                    if (sphere_node<kLds>(view, inv, oct, best_t, nlo, nhi, node, leaf, node_tests))
                         sphere_leaf(p, view, org, dir, inv, leaf, best_t, best_i, bnd, nlo, nhi,
                                     sph_tests);
                 } while (node != kEnd && (!kStep || --budget != 0));
