@@ -415,7 +415,7 @@ __device__ __forceinline__ bool tri_begin(const TraceParams &p, F3 org, F3 dir, 
 
 // One node of the triangle tree (static or camera-origin); an entered leaf is
 // handed back in `leaf` as (first << 3) | count, like sphere_node.
-__device__ __forceinline__ void tri_node(const TraceParams &p, F3 noi, F3 inv, F3 dlt, bool cam,
+__device__ __forceinline__ bool tri_node(const TraceParams &p, F3 noi, F3 inv, F3 dlt, bool cam,
                                          float rho, float cap, uint32_t &node,
                                          uint32_t &leaf, uint32_t &node_tests) {
     ++node_tests;
@@ -469,12 +469,15 @@ __device__ __forceinline__ void tri_node(const TraceParams &p, F3 noi, F3 inv, F
     widen(B0.z, B1.z, N0.z, N1.z, noi.z, inv.z, t0z, t1z);
     const float tn = fmaxf(fmaxf(fminf(t0x, t1x), fminf(t0y, t1y)), fminf(t0z, t1z));
     const float tf = fminf(fminf(fmaxf(t0x, t1x), fmaxf(t0y, t1y)), fmaxf(t0z, t1z));
-    const bool skip = tn > tf || tf < 0.001f || tn > cap;
+    // tn > cap as an integer compare (cap > 0 or +inf; see sphere_node: a
+    // NaN tn only comes from a NaN ray, which records no triangle)
+    const bool skip = tn > tf || tf < 0.001f || __float_as_int(tn) > __float_as_int(cap);
     // a: child | axis << 29, or leaf bit | first << 3 | count
     const bool is_leaf = (a & kLeafBitDev) != 0;
     const uint32_t child = a & 0x1FFFFFFFu;
     node = (skip || is_leaf) ? miss : child;
-    if (!skip && is_leaf) leaf = a & ~kLeafBitDev;
+    leaf = a & ~kLeafBitDev;  // read only when the flag is set
+    return !skip && is_leaf;
 }
 
 __device__ __forceinline__ void tri_leaf(const TraceParams &p, F3 org, F3 dir, bool cam,
@@ -821,9 +824,9 @@ __attribute__((amdgpu_waves_per_eu(RT_WAVES_PER_EU, 8))) void trace_kernel(Trace
                 const F3 dlt = f3(org.x - p.tbvh_oc[0], org.y - p.tbvh_oc[1], org.z - p.tbvh_oc[2]);
                 const F3 noi = f3(-(org.x * inv.x), -(org.y * inv.y), -(org.z * inv.z));
                 do {
-                    uint32_t leaf = 0;
-                    tri_node(p, noi, inv, dlt, cam, e, fminf(best_t, tri_t), node, leaf, tnode_tests);
-                    if (leaf != 0) tri_leaf(p, org, dir, cam, leaf, best_t, tri_t, tri_i, tri_in, tri_done);
+                    uint32_t leaf;
+                    if (tri_node(p, noi, inv, dlt, cam, e, fminf(best_t, tri_t), node, leaf, tnode_tests))
+                        tri_leaf(p, org, dir, cam, leaf, best_t, tri_t, tri_i, tri_in, tri_done);
                 } while (node != kNodeEndDev && (!kStep || --budget != 0));
                 if (node == kNodeEndDev) phase = kShade;
             }
