@@ -49,6 +49,17 @@ __device__ __forceinline__ bool xdiv_num3_ok(float a, float b, float c) {
     return (e >= -59) & (m < 0x1p60f);
 }
 
+// The same guard for numerators bounded by the denominator (|a| <= b (1 +
+// 2^-22), as the components of a vector are by its computed length): with b
+// <= 2^40 the upper bound holds by itself, so only the exponents are checked
+// (0 and inf/NaN have frexp exponent 0; inf/NaN components make the length
+// fail xdiv_den_ok).
+__device__ __forceinline__ bool xdiv_num3_small_ok(float a, float b, float c) {
+    const int e = min(min(__builtin_amdgcn_frexp_expf(a), __builtin_amdgcn_frexp_expf(b)),
+                      __builtin_amdgcn_frexp_expf(c));
+    return e >= -59;
+}
+
 // RN(1/b) for b in the guarded range (exhaustively checked, see above).
 __device__ __forceinline__ float xdiv_rcp(float b) {
     const float y0 = __builtin_amdgcn_rcpf(b);

@@ -64,7 +64,14 @@ __device__ __forceinline__ F3 divide_by(F3 a, float b) {
 }
 __device__ __forceinline__ F3 unit(F3 a) {  // NVec3::new, maths.rs:111-118
     const float len = xsqrt((a.x * a.x + a.y * a.y) + a.z * a.z);
-    return divide_by(a, len);
+#ifndef RT_NO_XDIV
+    // components are bounded by the length: the cheaper numerator guard
+    if (__builtin_expect((unsigned)xdiv_den_ok(len) & (unsigned)xdiv_num3_small_ok(a.x, a.y, a.z), 1)) {
+        const float y = xdiv_rcp(len);
+        return F3{xdiv(a.x, len, y), xdiv(a.y, len, y), xdiv(a.z, len, y)};
+    }
+#endif
+    return F3{a.x / len, a.y / len, a.z / len};
 }
 
 // xorshift32 (random.rs:22-30) and `x as f32 / u32::MAX as f32` == x * 2^-32.
