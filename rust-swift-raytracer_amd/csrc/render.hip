@@ -203,9 +203,9 @@ constexpr float kErrK = 3.0e-3f;  // >= 2.7x the derived sqrt(30u) = 1.12e-3 (DE
 // Where the traversal reads the tree from: global memory (any size) or the
 // workgroup's LDS copy (staged once per persistent workgroup).
 struct BvhView {
-    const float4 *nodes;     // 2 per node
+    const float4 *nodes;     // global: 2 per node; LDS: 48-B records (box | 8 x u16 links)
     const uint32_t *miss32;  // global: 8 x u32 per node
-    const uint16_t *miss16;  // LDS: 8 x u16 per node
+    const uint16_t *miss16;  // (unused: the LDS links live in the node records)
     const float4 *prims;
     const uint32_t *ids;
     const float4 *shade;     // per-sphere shading records (2 x float4)
@@ -256,13 +256,32 @@ __device__ __forceinline__ void spheres_big(const TraceParams &p, F3 org, F3 dir
 // sphere_leaf.  (Deferring leaf tests until every lane of the wave has one
 // pending -- "while-while" -- measured 6% slower on C2 and 60% on C5.)
 template <bool kLds>
-__device__ __forceinline__ bool sphere_node(const BvhView &v, F3 inv, uint32_t oct, float best_t,
-                                            F3 nlo, F3 nhi, uint32_t &node, uint32_t &leaf,
-                                            uint32_t &node_tests) {
+__device__ __forceinline__ bool sphere_node(const BvhView &v, F3 inv, uint32_t oct, uint32_t octm,
+                                            float best_t, F3 nlo, F3 nhi, uint32_t &node,
+                                            uint32_t &leaf, uint32_t &node_tests) {
     ++node_tests;
-    const float4 B0 = v.nodes[2 * node];
-    const float4 B1 = v.nodes[2 * node + 1];
-    const uint32_t miss = kLds ? (uint32_t)v.miss16[8 * node + oct] : v.miss32[8 * node + oct];
+    // LDS copy: `node` is the record's LDS byte address (48-B records: box | 8
+    // u16 links; links and child words are staged as addresses), so the box
+    // needs no address arithmetic and the link one add
+    float4 B0, B1;
+    uint32_t miss;
+    if (kLds) {
+#if defined(__HIP_DEVICE_COMPILE__)
+        // `node` is the record's LDS address (staged as such: no base add)
+        typedef const __attribute__((address_space(3))) char *lds_cptr;
+        const lds_cptr rec = (lds_cptr)(uintptr_t)node;
+        B0 = *(const __attribute__((address_space(3))) float4 *)rec;
+        B1 = *(const __attribute__((address_space(3))) float4 *)(rec + 16);
+        miss = *(const __attribute__((address_space(3))) uint16_t *)(rec + 32 + 2 * oct);
+#else
+        B0 = B1 = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        miss = 0;
+#endif
+    } else {
+        B0 = v.nodes[2 * node];
+        B1 = v.nodes[2 * node + 1];
+        miss = v.miss32[8 * node + oct];
+    }
     // Slab values b * inv - lo * inv as one fma each, nlo = -(lo * inv) per ray
     // (sphere_slabs): the result is the exact slab value of a face moved by
     // <= u|lo| + 3u|b - lo| (rounded lo * inv, rcp, the fma's rounding), which
@@ -284,7 +303,11 @@ __device__ __forceinline__ bool sphere_node(const BvhView &v, F3 inv, uint32_t o
     const bool skip = tn > tf || tf < 0.001f || __float_as_int(tn) > __float_as_int(best_t);
     const uint32_t a = __float_as_uint(B0.w);
     const bool is_leaf = (a & kLeafBitDev) != 0;
-    const uint32_t child = a + ((oct >> __float_as_uint(B1.w)) & 1u);  // near child first
+    // near child first: with kLds the staged axis word is 8 * axis and octm
+    // holds 48 * (octant bit) per axis in bytes 0..2, so the right child's
+    // record (+48) is one bit-field extract away
+    const uint32_t child = kLds ? a + __builtin_amdgcn_ubfe(octm, __float_as_uint(B1.w), 8)
+                                : a + ((oct >> __float_as_uint(B1.w)) & 1u);
     node = (skip || is_leaf) ? miss : child;
     // (returned as a flag, so the caller branches on it directly; leaf is only
     // read when it is set)
@@ -635,16 +658,40 @@ __attribute__((amdgpu_waves_per_eu(RT_WAVES_PER_EU, 8))) void trace_kernel(Trace
     const uint32_t lane = __lane_id();
     extern __shared__ float4 lds[];
     BvhView view;
+    uint32_t sph_root = 0;  // the sphere walk's first node (its LDS address with kLds)
     if (kLds) {
-        // layout: nodes (2 x float4 / node) | prims (float4) | shade (2 x float4 /
-        // sphere) | ids (u32) | kinds (u32) | miss (8 x u16 / node)
+        // layout: node records (48 B: box float4 x 2 | 8 x u16 links) | prims
+        // (float4) | shade (2 x float4 / sphere) | ids (u32) | kinds (u32).
+        // Node references become record LDS addresses (base + index * 48; the
+        // kernel has no static LDS, so base is 0 and they stay below 65520: the
+        // copy holds < 1366 nodes); 0xFFFF stays the end marker.
         float4 *n4 = lds;
-        float4 *p4 = n4 + 2 * p.nnodes;
+        const uint32_t lbase = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) float4 *)lds;
+        sph_root = lbase;
+        float4 *p4 = n4 + 3 * p.nnodes;
         float4 *s4 = p4 + p.nprims;
         uint32_t *id = reinterpret_cast<uint32_t *>(s4 + 2 * p.nsph_padded);
         uint32_t *kd = id + p.nprims;
-        uint32_t *m32 = kd + p.nsph_padded;  // miss16 viewed as u32 words (4 per node)
-        for (uint32_t i = threadIdx.x; i < 2 * p.nnodes; i += blockDim.x) n4[i] = p.bvh_nodes[i];
+        const uint16_t *g16 = p.bvh_miss16;
+        for (uint32_t i = threadIdx.x; i < p.nnodes; i += blockDim.x) {
+            float4 b0 = p.bvh_nodes[2 * i];
+            const uint32_t a = __float_as_uint(b0.w);
+            float4 b1 = p.bvh_nodes[2 * i + 1];
+            if (!(a & kLeafBitDev)) {
+                b0.w = __uint_as_float(lbase + a * 48u);                 // left child's record
+                b1.w = __uint_as_float(8u * __float_as_uint(b1.w));      // split axis * 8
+            }
+            n4[3 * i] = b0;
+            n4[3 * i + 1] = b1;
+            uint32_t w[4];
+            for (int k = 0; k < 4; ++k) {
+                const uint32_t l0 = g16[8 * i + 2 * k], l1 = g16[8 * i + 2 * k + 1];
+                w[k] = (l0 == 0xFFFFu ? 0xFFFFu : lbase + l0 * 48u) |
+                       ((l1 == 0xFFFFu ? 0xFFFFu : lbase + l1 * 48u) << 16);
+            }
+            n4[3 * i + 2] = make_float4(__uint_as_float(w[0]), __uint_as_float(w[1]),
+                                        __uint_as_float(w[2]), __uint_as_float(w[3]));
+        }
         for (uint32_t i = threadIdx.x; i < p.nprims; i += blockDim.x) {
             p4[i] = p.bvh_prims[i];
             id[i] = p.bvh_prim_id[i];
@@ -654,10 +701,8 @@ __attribute__((amdgpu_waves_per_eu(RT_WAVES_PER_EU, 8))) void trace_kernel(Trace
             s4[2 * i + 1] = p.sph_shade[2 * i + 1];
             kd[i] = p.sph_kind[i];
         }
-        const uint32_t *g16 = reinterpret_cast<const uint32_t *>(p.bvh_miss16);
-        for (uint32_t i = threadIdx.x; i < 4 * p.nnodes; i += blockDim.x) m32[i] = g16[i];
         __syncthreads();
-        view = BvhView{n4, nullptr, reinterpret_cast<const uint16_t *>(m32), p4, id, s4, kd};
+        view = BvhView{n4, nullptr, nullptr, p4, id, s4, kd};
     } else {
         view = BvhView{p.bvh_nodes, p.bvh_miss, nullptr, p.bvh_prims, p.bvh_prim_id,
                        p.sph_shade, p.sph_kind};
@@ -764,7 +809,7 @@ __attribute__((amdgpu_waves_per_eu(RT_WAVES_PER_EU, 8))) void trace_kernel(Trace
                     best_i = -1;
                     if (kBvh) {
                         spheres_big(p, org, dir, best_t, best_i);
-                        node = 0;
+                        node = sph_root;
                         // (RT_AMD_ABLATE=1: timing-only diagnostic, results are wrong)
                         phase = (p.ablate & 1u) ? kTriInit : kSph;
                         if (!kMesh && bounce == 0 && (spl1 >> 16) != kSphListWalk) {
@@ -795,9 +840,12 @@ __attribute__((amdgpu_waves_per_eu(RT_WAVES_PER_EU, 8))) void trace_kernel(Trace
                 const SphBound bnd = sph_bound(p, org);
                 F3 nlo, nhi;
                 sphere_slabs(org, inv, sph_inflation(p, bnd, best_t), nlo, nhi);
+                const uint32_t octm = ((oct & 1u) ? 48u : 0u) | ((oct & 2u) ? 48u << 8 : 0u) |
+                                      ((oct & 4u) ? 48u << 16 : 0u);
                 do {
                     uint32_t leaf;
-                    if (sphere_node<kLds>(view, inv, oct, best_t, nlo, nhi, node, leaf, node_tests))
+                    if (sphere_node<kLds>(view, inv, oct, octm, best_t, nlo, nhi, node, leaf,
+                                          node_tests))
                         sphere_leaf(p, view, org, dir, inv, leaf, best_t, best_i, bnd, nlo, nhi,
                                     sph_tests);
                 } while (node != kEnd && (!kStep || --budget != 0));

@@ -143,7 +143,8 @@ static int device_for(WorldState &w, int want, DeviceState *&out) {
             TraceParams lp{};
             lp.nnodes = d->nnodes; lp.nprims = d->nprims; lp.nsph_padded = (uint32_t)p.nsph_padded;
             const size_t lds = trace_lds_bytes(lp);
-            if (d->nnodes < 0xFFFF && lds <= env_u64("RT_AMD_LDS_MAX", 64 * 1024)) {
+            // (the LDS copy addresses 48-B node records with u16 byte offsets)
+            if (d->nnodes <= 65520 / 48 && lds <= env_u64("RT_AMD_LDS_MAX", 64 * 1024)) {
                 std::vector<uint16_t> m16(bv.miss.size());
                 for (size_t i = 0; i < m16.size(); ++i)
                     m16[i] = bv.miss[i] == kNodeEnd ? (uint16_t)0xFFFF : (uint16_t)bv.miss[i];
