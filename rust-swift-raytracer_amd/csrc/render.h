@@ -103,7 +103,9 @@ hipError_t launch_resolve_ex(const float *samples, uint32_t *out, uint32_t npix,
                              hipStream_t stream);
 // variant: 0 brute force, 1 BVH from global memory, 2 BVH staged in LDS;
 // step: the sliced-walk kernel (TraceParams::step); tri: the scene has triangles
-hipError_t trace_occupancy(int *blocks_per_cu, int variant, size_t lds_bytes, bool step, bool tri);
+// workgroups per CU of one trace_kernel instance (count: the counting variant)
+hipError_t trace_occupancy(int *blocks_per_cu, int variant, size_t lds_bytes, bool step, bool tri,
+                           bool count);
 size_t trace_lds_bytes(const TraceParams &p);
 // threads per trace workgroup: LDS-tree kernels (sphere-only scenes or not) vs global
 uint32_t trace_block_threads(bool lds, bool mesh);

@@ -644,6 +644,14 @@ __device__ __forceinline__ void resolve_chunk(const TraceParams &p, const float 
 #ifndef RT_WAVES_PER_EU
 #define RT_WAVES_PER_EU 6
 #endif
+// The lean (uncounted) triangle-scene kernels run at 8 waves per SIMD (64
+// VGPRs, 4 workgroups of 512 per CU): their sliced walks are latency-bound
+// on the triangle loads, and the extra waves hide it (A/B on C5: 6 -> 272 ms,
+// 7 -> 274, 8 -> 264).  The counting variants keep 6 (at 8 their counters
+// spill: 298 ms).
+#ifndef RT_WAVES_PER_EU_MESH
+#define RT_WAVES_PER_EU_MESH 8
+#endif
 // LDS workgroup of the sphere-only kernel.  Measured on C2 (A/B, one
 // process): 512 -> 6.77 ms, 768 -> 6.73, 896 -> 8.41, 1024 (8 waves/SIMD)
 // -> 7.78; above 6 waves per SIMD the per-wave ray state thrashes the L1.
@@ -654,7 +662,8 @@ __device__ __forceinline__ void resolve_chunk(const TraceParams &p, const float 
 // away, which keeps the sphere-only kernel's register allocation small).
 template <bool kBvh, bool kLds, bool kStep, bool kMesh, bool kCount>
 __global__ __launch_bounds__(kLds ? (kMesh ? 512 : RT_LDS_BLOCK_SPHERES) : 256)
-__attribute__((amdgpu_waves_per_eu(RT_WAVES_PER_EU, 8))) void trace_kernel(TraceParams p) {
+__attribute__((amdgpu_waves_per_eu((kMesh && !kCount) ? RT_WAVES_PER_EU_MESH : RT_WAVES_PER_EU, 8)))
+void trace_kernel(TraceParams p) {
     const uint32_t lane = __lane_id();
     extern __shared__ float4 lds[];
     BvhView view;
@@ -1244,25 +1253,33 @@ hipError_t launch_resolve_ex(const float *samples, uint32_t *out, uint32_t npix,
     return hipGetLastError();
 }
 
-template <bool kStep, bool kMesh>
+template <bool kStep, bool kMesh, bool kCount>
 static hipError_t trace_occupancy_t(int *blocks_per_cu, int variant, size_t lds_bytes) {
     if (variant == 2)
         return hipOccupancyMaxActiveBlocksPerMultiprocessor(
-            blocks_per_cu, trace_kernel<true, true, kStep, kMesh, true>, trace_block_threads(true, kMesh),
-            lds_bytes);
+            blocks_per_cu, trace_kernel<true, true, kStep, kMesh, kCount>,
+            trace_block_threads(true, kMesh), lds_bytes);
     if (variant == 1)
         return hipOccupancyMaxActiveBlocksPerMultiprocessor(
-            blocks_per_cu, trace_kernel<true, false, kStep, kMesh, true>, 256, 0);
+            blocks_per_cu, trace_kernel<true, false, kStep, kMesh, kCount>, 256, 0);
     return hipOccupancyMaxActiveBlocksPerMultiprocessor(
-        blocks_per_cu, trace_kernel<false, false, kStep, kMesh, true>, 256, 0);
+        blocks_per_cu, trace_kernel<false, false, kStep, kMesh, kCount>, 256, 0);
 }
 
-hipError_t trace_occupancy(int *blocks_per_cu, int variant, size_t lds_bytes, bool step, bool tri) {
+template <bool kCount>
+static hipError_t trace_occupancy_c(int *blocks_per_cu, int variant, size_t lds_bytes, bool step,
+                                    bool tri) {
     if (step)
-        return tri ? trace_occupancy_t<true, true>(blocks_per_cu, variant, lds_bytes)
-                   : trace_occupancy_t<true, false>(blocks_per_cu, variant, lds_bytes);
-    return tri ? trace_occupancy_t<false, true>(blocks_per_cu, variant, lds_bytes)
-               : trace_occupancy_t<false, false>(blocks_per_cu, variant, lds_bytes);
+        return tri ? trace_occupancy_t<true, true, kCount>(blocks_per_cu, variant, lds_bytes)
+                   : trace_occupancy_t<true, false, kCount>(blocks_per_cu, variant, lds_bytes);
+    return tri ? trace_occupancy_t<false, true, kCount>(blocks_per_cu, variant, lds_bytes)
+               : trace_occupancy_t<false, false, kCount>(blocks_per_cu, variant, lds_bytes);
+}
+
+hipError_t trace_occupancy(int *blocks_per_cu, int variant, size_t lds_bytes, bool step, bool tri,
+                           bool count) {
+    return count ? trace_occupancy_c<true>(blocks_per_cu, variant, lds_bytes, step, tri)
+                 : trace_occupancy_c<false>(blocks_per_cu, variant, lds_bytes, step, tri);
 }
 
 }  // namespace rtamd

@@ -97,10 +97,11 @@ static int device_for(WorldState &w, int want, DeviceState *&out) {
         HIP_TRY(hipGetDeviceProperties(&prop, dev));
         d->num_cus = prop.multiProcessorCount;
         const bool tri = w.packed.ntri > 0;  // the kTri kernels (render.hip)
-        for (int st = 0; st < 2; ++st) {
-            HIP_TRY(trace_occupancy(&d->blocks_per_cu[st], 0, 0, st, tri));
-            HIP_TRY(trace_occupancy(&d->blocks_per_cu_bvh[st], 1, 0, st, tri));
-        }
+        for (int c = 0; c < 2; ++c)
+            for (int st = 0; st < 2; ++st) {
+                HIP_TRY(trace_occupancy(&d->blocks_per_cu[c][st], 0, 0, st, tri, c));
+                HIP_TRY(trace_occupancy(&d->blocks_per_cu_bvh[c][st], 1, 0, st, tri, c));
+            }
         // scene upload (once per device)
         const PackedScene &p = w.packed;
         auto up = [&](void **dst, const std::vector<float> &src) -> hipError_t {
@@ -150,9 +151,13 @@ static int device_for(WorldState &w, int want, DeviceState *&out) {
                     m16[i] = bv.miss[i] == kNodeEnd ? (uint16_t)0xFFFF : (uint16_t)bv.miss[i];
                 HIP_TRY(hipMalloc((void **)&d->bvh_miss16, m16.size() * 2));
                 HIP_TRY(hipMemcpy(d->bvh_miss16, m16.data(), m16.size() * 2, hipMemcpyHostToDevice));
-                for (int st = 0; st < 2; ++st)
-                    HIP_TRY(trace_occupancy(&d->blocks_per_cu_lds[st], 2, lds, st, tri));
-                if (d->blocks_per_cu_lds[0] > 0 && d->blocks_per_cu_lds[1] > 0) d->lds_bytes = lds;
+                bool fits = true;
+                for (int c = 0; c < 2; ++c)
+                    for (int st = 0; st < 2; ++st) {
+                        HIP_TRY(trace_occupancy(&d->blocks_per_cu_lds[c][st], 2, lds, st, tri, c));
+                        fits = fits && d->blocks_per_cu_lds[c][st] > 0;
+                    }
+                if (fits) d->lds_bytes = lds;
             }
         }
         const TriangleBVH &tb = w.tbvh;
@@ -170,11 +175,14 @@ static int device_for(WorldState &w, int want, DeviceState *&out) {
             d->tloose = (uint32_t)tb.loose.size();
         }
         const uint64_t bpc = env_u64("RT_AMD_BLOCKS_PER_CU", 0);
-        for (int st = 0; st < 2; ++st) {
-            if (bpc) d->blocks_per_cu[st] = d->blocks_per_cu_bvh[st] = d->blocks_per_cu_lds[st] = (int)bpc;
-            d->blocks_per_cu[st] = std::max(d->blocks_per_cu[st], 1);
-            d->blocks_per_cu_bvh[st] = std::max(d->blocks_per_cu_bvh[st], 1);
-        }
+        for (int c = 0; c < 2; ++c)
+            for (int st = 0; st < 2; ++st) {
+                if (bpc)
+                    d->blocks_per_cu[c][st] = d->blocks_per_cu_bvh[c][st] = d->blocks_per_cu_lds[c][st] =
+                        (int)bpc;
+                d->blocks_per_cu[c][st] = std::max(d->blocks_per_cu[c][st], 1);
+                d->blocks_per_cu_bvh[c][st] = std::max(d->blocks_per_cu_bvh[c][st], 1);
+            }
         HIP_TRY(hipMalloc((void **)&d->counter, kMaxParts * 128));
         slot = std::move(d);
     }
@@ -416,12 +424,15 @@ int render_frame(WorldState &w, const CameraModel &cam, size_t width, size_t hei
     // 32 -> 6.10); sliced walks refill every iteration (C5: 32 costs +5 %)
     p.refill_min = (uint32_t)std::max<uint64_t>(1, env_u64("RT_AMD_REFILL", p.step ? 1 : 32));
     const int sv = p.step ? 1 : 0;
-    const int bpc = !use_bvh ? d->blocks_per_cu[sv] : p.use_lds ? d->blocks_per_cu_lds[sv] : d->blocks_per_cu_bvh[sv];
+    const bool timed = stats != nullptr;  // HIP-event timing + counters need a host wait
+    const int ctv = timed ? 1 : 0;         // launch_trace runs the counting variant iff p.stats
+    const int bpc = !use_bvh   ? d->blocks_per_cu[ctv][sv]
+                    : p.use_lds ? d->blocks_per_cu_lds[ctv][sv]
+                                : d->blocks_per_cu_bvh[ctv][sv];
     const uint64_t waves_per_block = trace_block_threads(use_bvh && p.use_lds, p.ntri != 0) / 64;
     const uint64_t full_blocks = (uint64_t)bpc * (uint64_t)d->num_cus;
     double trace_ms = 0.0, resolve_ms = 0.0;
     uint32_t launches = 0, waves = 0;
-    const bool timed = stats != nullptr;  // HIP-event timing + counters need a host wait
     // counters only when asked for: one 16-slot record per wave, summed here
     const uint64_t max_waves = full_blocks * waves_per_block;
     p.stats = nullptr;
