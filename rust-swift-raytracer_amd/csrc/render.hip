@@ -570,15 +570,15 @@ __device__ __forceinline__ void resolve_store(const TraceParams &p, uint32_t lp,
 // (common.rs:333-341, the same fold as resolve_kernel).  The samples were
 // stored by this wave: a workgroup-scope fence orders them (one CU, one L1).
 //
-// L lanes per pixel (a power of two, L * pixels <= 64): per round, lane j of
-// pixel g's group loads samples 4j .. 4j+3 of the round's 4L (one float4 per
-// plane, all loads of the round in flight together), then every lane of the
-// group folds the group's 4L values in sample order through ds_bpermute, so
-// the fold's latency is one load round trip per round instead of one per
-// float4.  Chunks whose spp does not split this way, and the triangle
-// kernels (kGroup false: at the VGPR cap the group fold adds scratch; C5
-// +0.7 %), sum one pixel per lane (C2: -0.6 % for the group fold).
-template <bool kGroup>
+// One lane per (pixel, plane) when 3 * pixels <= 64 and spp % 4 == 0: lane
+// c * np + g folds plane c of pixel g in sample order from float4 loads (4
+// in flight per round), then the pixel's lane collects the G and B sums with
+// two shuffles: spp adds and spp / 4 loads per lane (A/B on C2 -1.7 %
+// against folding float4 groups through ds_bpermute, 3 * spp bpermutes and
+// adds per pixel).  Other chunks, and the triangle kernels (kPlaneLanes
+// false: at their 64-VGPR cap the float4 rounds spill, C5 +7 %), sum one
+// pixel per lane.
+template <bool kPlaneLanes>
 __device__ __forceinline__ void resolve_chunk(const TraceParams &p, const float *ring, uint32_t plane,
                                               uint32_t off, uint32_t base, uint32_t len,
                                               uint32_t lane) {
@@ -586,37 +586,32 @@ __device__ __forceinline__ void resolve_chunk(const TraceParams &p, const float 
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
     const uint32_t spp = p.spp;
     const uint32_t np = fdiv(len, p.div_spp), pix0 = fdiv(base, p.div_spp);
-    uint32_t sh = 0;  // L = 2^sh: 4L | spp, L * np <= 64
-    while ((2u << sh) * np <= kWave && spp % (8u << sh) == 0) ++sh;
-    if (kGroup && sh > 0 && (spp & 3u) == 0) {
-        const uint32_t L = 1u << sh, step = 4u * L;
-        const uint32_t g = lane >> sh, j = lane & (L - 1u);
-        const bool on = g < np;
-        const float *src = ring + off + (on ? g * spp : 0u) + 4u * j;
-        const float4 z = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-        auto ld = [&](uint32_t k, float4 &R, float4 &G, float4 &B) {
-            R = G = B = z;
-            if (on) {
-                R = *reinterpret_cast<const float4 *>(src + k);
-                G = *reinterpret_cast<const float4 *>(src + plane + k);
-                B = *reinterpret_cast<const float4 *>(src + 2 * plane + k);
+    if (kPlaneLanes && 3u * np <= kWave && (spp & 3u) == 0) {
+        const uint32_t c = lane >= np ? (lane >= 2u * np ? 2u : 1u) : 0u;
+        const uint32_t g = lane - c * np;
+        const bool on = lane < 3u * np;
+        const float *src = ring + off + c * plane + (on ? g : 0u) * spp;
+        float acc = 0.0f;
+        for (uint32_t k = 0; k < spp; k += 16u) {
+            float4 v[4];
+#pragma unroll
+            for (uint32_t q = 0; q < 4; ++q) {
+                v[q] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+                if (on && k + 4u * q < spp) v[q] = *reinterpret_cast<const float4 *>(src + k + 4u * q);
             }
-        };
-        float ar = 0.0f, ag = 0.0f, ab = 0.0f;
-        for (uint32_t k = 0; k < spp; k += step) {
-            float4 R, G, B;
-            ld(k, R, G, B);
-            for (uint32_t t = 0; t < L; ++t) {
-                const int sl = (int)((g << sh) + t);
-                ar = ar + __shfl(R.x, sl); ar = ar + __shfl(R.y, sl);
-                ar = ar + __shfl(R.z, sl); ar = ar + __shfl(R.w, sl);
-                ag = ag + __shfl(G.x, sl); ag = ag + __shfl(G.y, sl);
-                ag = ag + __shfl(G.z, sl); ag = ag + __shfl(G.w, sl);
-                ab = ab + __shfl(B.x, sl); ab = ab + __shfl(B.y, sl);
-                ab = ab + __shfl(B.z, sl); ab = ab + __shfl(B.w, sl);
+#pragma unroll
+            for (uint32_t q = 0; q < 4; ++q) {
+                if (k + 4u * q < spp) {  // (wave-uniform)
+                    acc = acc + v[q].x;
+                    acc = acc + v[q].y;
+                    acc = acc + v[q].z;
+                    acc = acc + v[q].w;
+                }
             }
         }
-        if (on && j == 0) resolve_store(p, pix0 + g, ar, ag, ab);
+        const float sg = __shfl(acc, (int)(lane < np ? np + lane : lane));
+        const float sb = __shfl(acc, (int)(lane < np ? 2u * np + lane : lane));
+        if (lane < np) resolve_store(p, pix0 + lane, acc, sg, sb);
         return;
     }
     for (uint32_t i = lane; i < np; i += kWave) {
