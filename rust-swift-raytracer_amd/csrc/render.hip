@@ -639,13 +639,13 @@ __device__ __forceinline__ void resolve_chunk(const TraceParams &p, const float 
 #ifndef RT_WAVES_PER_EU
 #define RT_WAVES_PER_EU 6
 #endif
-// The lean (uncounted) triangle-scene kernels run at 8 waves per SIMD (64
-// VGPRs, 4 workgroups of 512 per CU): their sliced walks are latency-bound
-// on the triangle loads, and the extra waves hide it (A/B on C5: 6 -> 272 ms,
-// 7 -> 274, 8 -> 264).  The counting variants keep 6 (at 8 their counters
-// spill: 298 ms).
+// Waves per SIMD of the lean (uncounted) triangle-scene kernels.  A/B on C5:
+// with 256-node walk slices 8 waves beat 6 (264 vs 272 ms; 7: 274), with
+// 128- or 96-node slices 6 waves win again (242 / 240 vs 248 / 251 ms at 8).
+// The counting variants use RT_WAVES_PER_EU; the host queries occupancy per
+// variant (trace_occupancy).
 #ifndef RT_WAVES_PER_EU_MESH
-#define RT_WAVES_PER_EU_MESH 8
+#define RT_WAVES_PER_EU_MESH 6
 #endif
 // LDS workgroup of the sphere-only kernel.  Measured on C2 (A/B, one
 // process): 512 -> 6.77 ms, 768 -> 6.73, 896 -> 8.41, 1024 (8 waves/SIMD)

@@ -310,10 +310,10 @@ int render_frame(WorldState &w, const CameraModel &cam, size_t width, size_t hei
     p.div_width = make_fastdiv((uint32_t)width);
     p.div_spp = make_fastdiv(spp ? spp : 1);
     p.div_rowblock = make_fastdiv(B);
-    // node visits per lane per loop iteration of a sliced walk (C5 at 8 waves
-    // per SIMD, A/B: 32 -> 277 ms, 64 -> 259, 96 -> 252, 128 -> 248, 192 ->
-    // 251, 256 -> 263, 512 -> 353)
-    p.steps = (uint32_t)std::max<uint64_t>(1, env_u64("RT_AMD_STEPS", 128));
+    // node visits per lane per loop iteration of a sliced walk (A/B on C5, 8
+    // waves per SIMD: 32 -> 277 ms, 64 -> 259, 96 -> 252, 128 -> 248, 192 ->
+    // 251, 256 -> 263, 512 -> 353; 6 waves: 64 -> 243, 96 -> 240, 128 -> 242)
+    p.steps = (uint32_t)std::max<uint64_t>(1, env_u64("RT_AMD_STEPS", 96));
     p.row_block = B; p.rank = o.rank; p.nranks = nranks;
     const bool use_bvh = d->nnodes > 0 && o.accel != RT_ACCEL_BRUTE;
     if (use_bvh) {
