@@ -152,11 +152,13 @@ def test_edge_cases(w, h, spp, depth):
     assert gst["rays"] == st["rays"]
 
 
-@pytest.mark.parametrize("spp", [1, 3, 64, 255, 257, 1000, 4097])
+@pytest.mark.parametrize("spp", [1, 3, 4, 12, 20, 64, 255, 257, 1000, 4097])
 def test_in_kernel_resolve_chunking(spp):
     """Chunk and ring geometry of the in-kernel resolve: spp below, at and
     above the 256-job chunk (1000: one pixel per 1024-sample ring slot) and
-    above 4096 (the slab path): bit-exact against the oracle."""
+    above 4096 (the slab path); 4, 12, 20, 64, 1000 take the sphere kernel's
+    plane-lane fold (spp % 4 == 0, partial 16-sample rounds for 4, 12, 20 and
+    1000): bit-exact against the oracle."""
     src = scene_text("rtow.txt")
     w, h = (24, 8) if spp < 1000 else (5, 3)
     img, st, _ = O.Scene(src).render(w, h, spp, 8, mode=O.RNG_COUNTER, nthreads=8)
