@@ -52,10 +52,12 @@ Rust_WorldHandle *load_world(const char *source) {
     const char *leaf = std::getenv("RT_AMD_LEAF");  // tuning knob: spheres per BVH leaf
     world->state.bvh = rtamd::build_sphere_bvh(world->state.scene.spheres,
                                                leaf ? (uint32_t)std::atoi(leaf) : 3u);
-    const char *tleaf = std::getenv("RT_AMD_TRI_LEAF");  // triangles per BVH leaf
+    // triangles per BVH leaf (A/B on C5 at 96-node walk slices: 1 -> 222 ms,
+    // 2 -> 240, 3 -> 293)
+    const char *tleaf = std::getenv("RT_AMD_TRI_LEAF");
     world->state.tbvh = rtamd::build_triangle_bvh(world->state.scene.triangles,
                                                   world->state.packed.tri_hot,
-                                                  tleaf ? (uint32_t)std::atoi(tleaf) : 2u);
+                                                  tleaf ? (uint32_t)std::atoi(tleaf) : 1u);
     // bounce-0 triangle tree for the scene camera (rebuilt by the first render
     // after move_camera_position, which does not see the world)
     rtamd::prepare_camera(world->state, world->state.scene.camera);
