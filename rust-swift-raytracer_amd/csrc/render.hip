@@ -647,11 +647,14 @@ __device__ __forceinline__ void resolve_chunk(const TraceParams &p, const float 
 #ifndef RT_WAVES_PER_EU_MESH
 #define RT_WAVES_PER_EU_MESH 6
 #endif
-// LDS workgroup of the sphere-only kernel.  Measured on C2 (A/B, one
-// process): 512 -> 6.77 ms, 768 -> 6.73, 896 -> 8.41, 1024 (8 waves/SIMD)
-// -> 7.78; above 6 waves per SIMD the per-wave ray state thrashes the L1.
+// LDS workgroup of the sphere-only kernel: 768 threads, 2 per CU (6 waves
+// per SIMD).  Measured on C2 (A/B, one process): 512 -> 6.77 ms, 768 -> 6.73,
+// 896 -> 8.41, 1024 (8 waves/SIMD) -> 7.78 (above 6 waves per SIMD the
+// per-wave ray state thrashes the L1); with the current kernel 256 -> 7.90,
+// 384 -> 6.15, 512 -> 5.42 = 768 at N = 1, and on the 8-rank tile 768 beats
+// 512 by 3 % (0.90 vs 0.93 ms).
 #ifndef RT_LDS_BLOCK_SPHERES
-#define RT_LDS_BLOCK_SPHERES 512
+#define RT_LDS_BLOCK_SPHERES 768
 #endif
 // kMesh: the scene has triangles (else the whole Mesh::hit stage compiles
 // away, which keeps the sphere-only kernel's register allocation small).
