@@ -656,10 +656,15 @@ __device__ __forceinline__ void resolve_chunk(const TraceParams &p, const float 
 #ifndef RT_LDS_BLOCK_SPHERES
 #define RT_LDS_BLOCK_SPHERES 768
 #endif
+// LDS workgroup of the triangle-scene kernels (A/B on C5: 256 -> 223 ms,
+// 512 -> 221, 768 -> 225)
+#ifndef RT_LDS_BLOCK_MESH
+#define RT_LDS_BLOCK_MESH 512
+#endif
 // kMesh: the scene has triangles (else the whole Mesh::hit stage compiles
 // away, which keeps the sphere-only kernel's register allocation small).
 template <bool kBvh, bool kLds, bool kStep, bool kMesh, bool kCount>
-__global__ __launch_bounds__(kLds ? (kMesh ? 512 : RT_LDS_BLOCK_SPHERES) : 256)
+__global__ __launch_bounds__(kLds ? (kMesh ? RT_LDS_BLOCK_MESH : RT_LDS_BLOCK_SPHERES) : 256)
 __attribute__((amdgpu_waves_per_eu((kMesh && !kCount) ? RT_WAVES_PER_EU_MESH : RT_WAVES_PER_EU, 8)))
 void trace_kernel(TraceParams p) {
     const uint32_t lane = __lane_id();
@@ -1198,7 +1203,7 @@ __global__ __launch_bounds__(kResolveWaves * 64) void resolve_kernel(
 }  // namespace
 
 uint32_t trace_block_threads(bool lds, bool mesh) {
-    return lds ? (mesh ? 512u : (uint32_t)RT_LDS_BLOCK_SPHERES) : 256u;
+    return lds ? (mesh ? (uint32_t)RT_LDS_BLOCK_MESH : (uint32_t)RT_LDS_BLOCK_SPHERES) : 256u;
 }
 
 size_t trace_lds_bytes(const TraceParams &p) {
