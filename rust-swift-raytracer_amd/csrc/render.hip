@@ -14,7 +14,7 @@
 // is persistent: its 64 lanes trace one bounce per loop iteration; a lane
 // whose path ends writes the sample colour to a per-sample slab in HBM and
 // takes the next job (ballot + mbcnt prefix, one atomic per chunk per wave on
-// one of 64 partitioned counters), so lanes never idle behind the longest path
+// one of 16-64 partitioned counters), so lanes never idle behind the longest path
 // of their wave.  World::hit goes through exact BVHs (spheres: staged in LDS;
 // triangles: phantom-aware static and camera-origin trees, primary strip
 // lists) whose visiting order provably returns the reference's hit; the
