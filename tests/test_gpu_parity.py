@@ -276,15 +276,16 @@ def test_scheduling_knobs_do_not_change_samples(monkeypatch, scene):
 
 @pytest.mark.parametrize("scene", ["rtow", "mesh_soup"])
 def test_tree_shape_knobs_do_not_change_samples(monkeypatch, scene):
-    """Leaf sizes of the sphere, triangle and camera trees and the SAH's
-    phantom scale are load-time knobs: they reshape the trees, never a
+    """Leaf sizes of the sphere, triangle and camera trees, the SAH's phantom
+    scale and the radius above which spheres stay out of the tree are
+    load-time knobs: they reshape the trees, never a
     sample (every frame equals the default build's, bit for bit)."""
     src = scene_text("rtow.txt") if scene == "rtow" else _triangle_scene(41, 400, spheres=40)
     w, h, spp = 96, 54, 4
     ref, _ = render_kept(R.World(src), w, h, spp, 8)
     for env in [dict(RT_AMD_LEAF="1"), dict(RT_AMD_LEAF="7"), dict(RT_AMD_TRI_LEAF="2"),
                 dict(RT_AMD_TRI_LEAF="7"), dict(RT_AMD_CAM_LEAF="1"), dict(RT_AMD_CAM_LEAF="5"),
-                dict(RT_AMD_TRI_PHANTOM="0.5")]:
+                dict(RT_AMD_TRI_PHANTOM="0.5"), dict(RT_AMD_BIG_K="2")]:
         for k, v in env.items():
             monkeypatch.setenv(k, v)
         out, _ = render_kept(R.World(src), w, h, spp, 8)
