@@ -6,8 +6,11 @@ from tools/scenes.py, synthetic and deterministic).  A step = one full frame:
 every pixel sample traced and resolved to RGBA8 in HBM (and, for N>1 GPUs,
 the row tiles gathered over RCCL).  The scene is uploaded before timing.
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c5]
-  torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU)
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c4|c5]
+      one process drives N GPUs through the library (RtRenderOptions.ndevices:
+      row tiles + RCCL ncclGather to device 0)
+  torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU; the
+      launcher's rank count must equal --gpus)
 
 Rank 0 prints one JSON line.  `roofline` prices the trace kernel against the
 FP32 vector peak (the path is VALU-bound), `cpu_baseline`
@@ -66,8 +69,22 @@ def executed_flops(st):
             + 60 * st["tri_in_range"] + 40 * st["rays"] + 20 * st["samples"])
 
 
+def _host_cpus():
+    """(threads the CPU legs may use, CPUs the host reports).  A GPU box shows
+    the whole machine's CPUs but grants this job a share of 16."""
+    nproc = os.cpu_count() or 1
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        avail = nproc
+    return max(1, min(16, avail)), nproc
+
+
 def cpu_baseline(src, W, H, spp, depth, budget_s):
-    """Oracle (reference serial-RNG semantics), 1 thread, row-cyclic sample."""
+    """Oracle on a bounded row-cyclic sample of the same frame: 1 thread in
+    SERIAL RNG mode (the reference's semantics and its single-threaded
+    ray_trace, common.rs:320-361), and all usable host cores in COUNTER mode
+    (rows dealt over threads)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
 
@@ -86,10 +103,22 @@ def cpu_baseline(src, W, H, spp, depth, budget_s):
     _, st, _ = scene.render(W, H, spp_s, depth, mode=O.RNG_SERIAL, row_begin=step // 2,
                             row_step=step, out=img)
     dt = time.perf_counter() - t
+    threads, nproc = _host_cpus()
+    # all cores: the same rows (COUNTER mode), about half the serial budget
+    step_mt = max(1, step // max(1, int(threads * 0.5)))
+    t = time.perf_counter()
+    _, st_mt, _ = scene.render(W, H, spp_s, depth, mode=O.RNG_COUNTER, row_begin=step_mt // 2,
+                               row_step=step_mt, nthreads=threads, out=img)
+    dt_mt = time.perf_counter() - t
     return {"value": st["rays"] / dt / 1e6, "unit": "Mrays/s", "cores": 1, "kind": "port",
             "sample": f"oracle SERIAL RNG, rows {step // 2}::{step} of {W}x{H} at spp {spp_s} "
                       f"({st['samples']} samples, {st['rays']} rays, {dt:.1f} s)",
-            "msamples_per_s": st["samples"] / dt / 1e6}
+            "msamples_per_s": st["samples"] / dt / 1e6,
+            "host_nproc": nproc,
+            "all_cores": {"value": st_mt["rays"] / dt_mt / 1e6, "unit": "Mrays/s",
+                          "threads": threads, "mode": "COUNTER",
+                          "sample": f"rows {step_mt // 2}::{step_mt} at spp {spp_s} "
+                                    f"({st_mt['rays']} rays, {dt_mt:.1f} s)"}}
 
 
 def main():
@@ -102,8 +131,94 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--accel", default="auto", choices=["auto", "brute", "bvh"])
     args = ap.parse_args()
-
+    launched = "WORLD_SIZE" in os.environ  # torchrun: one process per GPU
     world_size = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.gpus < 1:
+        sys.exit(f"bench.py: --gpus must be >= 1 (got {args.gpus})")
+    if launched and world_size != args.gpus:
+        sys.exit(f"bench.py: --gpus {args.gpus} but the launcher started {world_size} ranks")
+    if launched:
+        multi_process(args, world_size)
+    else:
+        single_process(args)
+
+
+def _setup(args):
+    make_scene, W, H, spp, depth = S.CONFIGS[args.config]
+    accel = {"auto": R.ACCEL_AUTO, "brute": R.ACCEL_BRUTE, "bvh": R.ACCEL_BVH}[args.accel]
+    src = make_scene()
+    return src, R.World(src), W, H, spp, depth, accel
+
+
+def _timed(args, step, stream, sync, barrier):
+    """W warmup frames, one counting frame, then K timed frames between
+    barrier + synchronize on both sides (HIP events around each frame's render
+    on the launch stream), then counting frames like the timed ones."""
+    for _ in range(args.warmup):
+        step(False)
+    st_warm = step(True)  # counters of one frame (the frame is identical every step)
+    sync()
+    barrier()
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+           for _ in range(args.steps)]
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        step(False, evs[k])
+    sync()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    stats = [step(True) for _ in range(max(1, min(args.steps, 3)))]
+    assert all(s["rays"] == st_warm["rays"] for s in stats), "frames must be identical"
+    # (a timed frame is one job-counter fill + the trace launches)
+    trace_ms = (sum(a.elapsed_time(b) for a, b in evs) / args.steps
+                / max(1, stats[-1]["trace_launches"]))
+    count_trace_ms = sum(s["trace_ms"] for s in stats) / max(1, sum(s["trace_launches"] for s in stats))
+    return st_warm, stats[-1], elapsed, trace_ms, count_trace_ms
+
+
+def single_process(args):
+    """N GPUs from this one process through the library's multi-device mode
+    (RtRenderOptions.ndevices): every device renders its row blocks, an RCCL
+    ncclGather (ncclCommInitAll communicator) collects the tiles on device 0
+    and a kernel assembles the frame there.  N = 1 runs the same path (the
+    gather is then a copy into the frame)."""
+    ngpu = args.gpus
+    if R.device_count() < ngpu:
+        sys.exit(f"bench.py: --gpus {ngpu} but only {R.device_count()} devices are visible")
+    torch.cuda.set_device(0)
+    ranks = R.comm_count(0, ngpu)
+    assert ranks == ngpu, f"RCCL communicator has {ranks} ranks, --gpus {ngpu}"
+    src, world, W, H, spp, depth, accel = _setup(args)
+    dev = torch.device("cuda", 0)
+    frame = torch.zeros(H * W * 4, dtype=torch.uint8, device=dev)
+    stream = torch.cuda.Stream(device=dev)
+    torch.cuda.set_stream(stream)
+
+    def step(with_stats, ev=None):
+        if ev is not None:
+            ev[0].record(stream)
+        st = world.render_device(W, H, frame.data_ptr(), stream.cuda_stream, spp=spp, depth=depth,
+                                 row_block=ROW_BLOCK, device=0, accel=accel, stats=with_stats,
+                                 ndevices=ngpu)
+        if ev is not None:
+            ev[1].record(stream)
+        return st
+
+    def sync():
+        for d in range(ngpu):
+            torch.cuda.synchronize(d)
+
+    st_warm, st0, elapsed, trace_ms, count_trace_ms = _timed(args, step, stream, sync, lambda: None)
+    rows = R.tile_rows(H, ROW_BLOCK, 0, ngpu) if ngpu > 1 else H
+    par = (f"row-tiles x{ngpu} (block {ROW_BLOCK}), one process, RCCL ncclGather "
+           f"({ranks} ranks) to device 0")
+    _report(args, src, world, W, H, spp, depth, st0, st_warm["rays"] * args.steps, elapsed,
+            trace_ms, count_trace_ms, ngpu, rows, par, {"rccl_ranks": ranks, "launch": "single process"})
+
+
+def multi_process(args, world_size):
+    """One rank per GPU (torch.distributed.run): each rank renders its row
+    tile, the tiles are all-gathered over RCCL (torch.distributed "nccl")."""
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     # rehearsal knobs for a 1-GPU box (never set by the driver): all ranks on
@@ -117,11 +232,9 @@ def main():
             dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
         else:
             dist.init_process_group(backend)
+        assert dist.get_world_size() == args.gpus, "process group size != --gpus"
 
-    make_scene, W, H, spp, depth = S.CONFIGS[args.config]
-    accel = {"auto": R.ACCEL_AUTO, "brute": R.ACCEL_BRUTE, "bvh": R.ACCEL_BVH}[args.accel]
-    src = make_scene()
-    world = R.World(src)
+    src, world, W, H, spp, depth, accel = _setup(args)
     nr = world_size
     rows = R.tile_rows(H, ROW_BLOCK, rank, nr) if nr > 1 else H
     max_rows = max(R.tile_rows(H, ROW_BLOCK, r, nr) for r in range(nr)) if nr > 1 else H
@@ -152,33 +265,10 @@ def main():
                 gathered.copy_(tiles.gather_any(tile.cpu(), nr))
         return st
 
-    for _ in range(args.warmup):
-        step(False)
-    st_warm = step(True)  # counters of one frame (the frame is identical every step)
-    torch.cuda.synchronize()
-    if nr > 1:
-        dist.barrier()
-    # HIP events (torch's current stream is the launch stream) around each
-    # timed frame's render: the trace kernel's launch duration for the roofline
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-           for _ in range(args.steps)]
-    t0 = time.perf_counter()
-    for k in range(args.steps):
-        step(False, evs[k])
-    torch.cuda.synchronize()
-    if nr > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    # work counters of frames like the timed ones (the counting kernel variant),
-    # right after the timed region
-    stats = [step(True) for _ in range(max(1, min(args.steps, 3)))]
-    assert all(s["rays"] == st_warm["rays"] for s in stats), "frames must be identical"
-
+    barrier = dist.barrier if nr > 1 else (lambda: None)
+    st_warm, st0, elapsed, trace_ms, count_trace_ms = _timed(
+        args, step, stream, torch.cuda.synchronize, barrier)
     rays = st_warm["rays"] * args.steps
-    # (a timed frame is one job-counter fill + the trace launches)
-    trace_ms = (sum(a.elapsed_time(b) for a, b in evs) / args.steps
-                / max(1, stats[-1]["trace_launches"]))
-    count_trace_ms = sum(s["trace_ms"] for s in stats) / max(1, sum(s["trace_launches"] for s in stats))
     if nr > 1:
         tdev = dev if backend == "nccl" else torch.device("cpu")
         t_max = torch.tensor([elapsed], dtype=torch.float64, device=tdev)
@@ -190,14 +280,19 @@ def main():
             # the assembled frame must equal a one-rank render (rehearsal check)
             img = tiles.assemble(gathered.cpu().numpy(), W, H, ROW_BLOCK, nr)
             if rank == 0:
-                ref, _ = world.render(W, H, spp, depth, accel=accel, device=local_rank)
+                ref, _ = world.render(W, H, spp, depth, device=local_rank)
                 assert (img == ref).all(), "assembled multi-rank frame differs"
                 print("verify: assembled frame == single-rank frame", file=sys.stderr)
-    if rank != 0:
+    if rank == 0:
+        par = f"row-tiles x{nr} (block {ROW_BLOCK}), one process per GPU, RCCL all-gather"
+        _report(args, src, world, W, H, spp, depth, st0, rays, elapsed, trace_ms, count_trace_ms,
+                nr, rows, par, {"rccl_ranks": nr, "launch": "torch.distributed.run"})
+    if nr > 1:
         dist.destroy_process_group()
-        return
 
-    st0 = stats[-1]
+
+def _report(args, src, world, W, H, spp, depth, st0, rays, elapsed, trace_ms, count_trace_ms,
+            nr, rows, parallelism, extra):
     launches = max(1, st0["trace_launches"])
     flops_per_launch = executed_flops(st0) / launches
     achieved_tflops = flops_per_launch / (trace_ms * 1e-3) / 1e12
@@ -227,7 +322,7 @@ def main():
         "config": {"workload": f"{args.config}: {W}x{H}, spp {spp}, depth {depth}, "
                                f"{world.num_spheres} spheres, {world.num_triangles} triangles, "
                                "COUNTER RNG", "width": W, "height": H, "spp": spp,
-                   "depth": depth, "parallelism": f"row-tiles x{nr} (block {ROW_BLOCK})"},
+                   "depth": depth, "parallelism": parallelism},
         "roofline": {"bound": "valu", "achieved": achieved_tflops,
                      "peak": FP32_VECTOR_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": achieved_tflops / FP32_VECTOR_PEAK_TFLOPS, "traffic": traffic,
@@ -246,11 +341,10 @@ def main():
                     "tri_in_range": st0["tri_in_range"] / st0["rays"],
                     "brute_force_sphere_tests": st0["sphere_tests"] / st0["rays"]},
     }
+    result.update(extra)
     if nr == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(src, W, H, spp, depth, args.cpu_seconds)
     print(json.dumps(result))
-    if nr > 1:
-        dist.destroy_process_group()
 
 
 if __name__ == "__main__":

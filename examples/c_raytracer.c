@@ -3,14 +3,19 @@
  * (Naxaes/Rust-Swift-Raytracer examples/c_raytracer.rs:48-62): load a world
  * through load_world, render a 200x200 frame through render (16 spp, depth 8,
  * lib.rs:51) and write it as an ASCII PPM (image.rs:59-81 format).
- * Uses only the reference ABI (include/raytracer.h).
+ * With no spp/depth arguments it uses only the reference ABI
+ * (include/raytracer.h).  With them (e.g. BASELINE configs[0], C1: 256x256,
+ * 1 spp, depth 4) it renders through the extension entry point rt_render_ex
+ * (include/raytracer_amd.h), because render() fixes 16/8 (lib.rs:51).
  *
- * usage: c_raytracer [out.ppm] [scene.txt] [width height]
+ * usage: c_raytracer [out.ppm] [scene.txt|-] [width height [spp depth]]
  */
 #include <stdio.h>
 #include <stdlib.h>
+#include <string.h>
 
 #include "raytracer.h"
+#include "raytracer_amd.h"
 
 /* The inline world of examples/c_raytracer.rs:15-44 (8 spheres, 2 triangles). */
 static const char *WORLD_SOURCE =
@@ -68,18 +73,32 @@ static int write_image(const Rust_CFramebuffer *fb, const char *path) {
 
 int main(int argc, char **argv) {
     const char *out = argc > 1 ? argv[1] : "examples/image.ppm";
-    char *scene = argc > 2 ? read_file(argv[2]) : NULL;
+    const int inline_world = argc <= 2 || strcmp(argv[2], "-") == 0;
+    char *scene = inline_world ? NULL : read_file(argv[2]);
     size_t width = argc > 4 ? (size_t)atol(argv[3]) : 200;
     size_t height = argc > 4 ? (size_t)atol(argv[4]) : 200;
-    if (argc > 2 && !scene) { fprintf(stderr, "cannot read %s\n", argv[2]); return 1; }
+    const int custom = argc > 6;
+    if (!inline_world && !scene) { fprintf(stderr, "cannot read %s\n", argv[2]); return 1; }
 
     Rust_ColorU8 *pixels = calloc(width * height, sizeof(Rust_ColorU8));
     Rust_WorldHandle *world = load_world(scene ? scene : WORLD_SOURCE);
     if (!world) { fprintf(stderr, "load_world failed\n"); return 1; }
 
     Rust_CFramebuffer fb = {width, height, pixels};
-    Rust_CFramebuffer result = render(fb, world);
-    if (!result.pixels) return 2;
+    Rust_CFramebuffer result = fb;
+    if (custom) {
+        RtRenderOptions opts;
+        rt_default_options(&opts);
+        opts.samples_per_pixel = atoi(argv[5]);
+        opts.max_ray_bounces = atoi(argv[6]);
+        if (rt_render_ex(fb, world, &opts, NULL) != 0) {
+            fprintf(stderr, "rt_render_ex failed: %s\n", rt_last_error());
+            return 2;
+        }
+    } else {
+        result = render(fb, world);
+        if (!result.pixels) return 2;
+    }
     if (write_image(&result, out) != 0) { fprintf(stderr, "cannot write %s\n", out); return 3; }
     printf("wrote %s (%zux%zu)\n", out, result.width, result.height);
     free(pixels);

@@ -38,6 +38,14 @@ typedef struct RtRenderOptions {
   int32_t device;                 /* HIP device ordinal, -1 = current device    */
   int32_t accel;                  /* RT_ACCEL_*: how World::hit finds spheres   */
   uint32_t flags;                 /* RT_FLAG_* (0 = default)                    */
+  int32_t ndevices;               /* 0: one device (`device`), this call renders
+                                     rank's tile.  >= 1: the WHOLE frame, row-
+                                     tiled (blocks of row_block rows) over
+                                     devices [first, first + ndevices), first =
+                                     `device` or the current device, in this one
+                                     process; an RCCL ncclGather (communicators
+                                     from ncclCommInitAll) collects the tiles on
+                                     the first device.  rank/nranks must be 0/1. */
 } RtRenderOptions;
 
 /* Frame resolve.  By default the trace kernel resolves each pixel itself: a
@@ -79,7 +87,10 @@ typedef struct RtRenderStats {
                                 (no slab, resolve_ms ~ 0)                    */
 } RtRenderStats;
 
-/* spp 16, depth 8 (lib.rs:51), COUNTER, seed 2547549, one rank, device -1. */
+/* spp 16, depth 8 (lib.rs:51), COUNTER, seed 2547549, one rank, device -1,
+ * row_block 8, ndevices 0.  render() applies the environment variable
+ * RT_AMD_DEVICES=N (N >= 1) as ndevices, so a C or Swift caller of the
+ * reference entry point can spread its frames over N GPUs. */
 void rt_default_options(RtRenderOptions *opts);
 
 /* Rows of a `height`-row image that belong to `rank` (see RtRenderOptions). */
@@ -96,8 +107,15 @@ uint32_t rt_sample_seed(uint32_t seed, uint64_t job);
 int rt_render_ex(Rust_CFramebuffer framebuffer, const Rust_WorldHandle *handle,
                  const RtRenderOptions *opts, RtRenderStats *stats);
 
+/* Threading: one frame at a time per handle.  Calls from several host threads
+ * on one handle are serialised by a lock; frames enqueued on different streams
+ * of one device are ordered (the later waits for the earlier: they share the
+ * device's scratch). */
+
 /* Same, but the tile is written to DEVICE memory `d_rgba` (rt_tile_rows*width
- * RGBA8) on HIP stream `hip_stream` (NULL = the library's stream).  The scene
+ * RGBA8; with ndevices >= 1 the whole width*height frame on the first device)
+ * on HIP stream `hip_stream` (NULL = the library's stream; with ndevices it is
+ * the first device's stream).  The scene
  * stays resident on the device between calls.  With `stats`, returns after the
  * frame is complete (HIP-event timings and counters filled in); with
  * stats == NULL the frame is only enqueued on the stream (no host wait), so
@@ -128,6 +146,13 @@ size_t rt_world_num_triangles(const Rust_WorldHandle *handle);
 int rt_world_sphere(const Rust_WorldHandle *handle, size_t i, float out[10]);
 /* v0 v1 v2 normal material(type, r, g, b, a, param) */
 int rt_world_triangle(const Rust_WorldHandle *handle, size_t i, float out[18]);
+/* Scene editing: replaces sphere / triangle i's material with (type, r, g,
+ * b, a, param), type 0 Diffuse, 1 Metal (param = fuzz), 2 Dielectric (param =
+ * ir), 3 Emission (materials.rs:7-12, 100-102; the scene grammar cannot
+ * produce Emission, parser.rs:175-234).  a must be 1.0 (every reference Color
+ * has alpha 1).  The next frame re-uploads the scene.  0 or -1. */
+int rt_world_set_sphere_material(Rust_WorldHandle *handle, size_t i, const float material[6]);
+int rt_world_set_triangle_material(Rust_WorldHandle *handle, size_t i, const float material[6]);
 /* origin, lower_left_corner, horizontal, vertical (camera.rs:8-15) */
 void rt_camera_get(const Rust_Camera *camera, float out[12]);
 /* ParseError discriminant of the last failed load_world (parser.rs:11-18),
@@ -139,6 +164,11 @@ int rt_write_ppm(const Rust_CFramebuffer *framebuffer, const char *path);
 
 /* Number of HIP devices visible (0 if the runtime is unavailable). */
 int rt_device_count(void);
+
+/* Rank count of the RCCL communicator that multi-device frames (ndevices =
+ * n, first device `first`, -1 = current) use; creates it on first use.
+ * Returns n, or a negative error (e.g. fewer than first + n devices). */
+int rt_comm_count(int first, int n);
 
 #ifdef __cplusplus
 }

@@ -52,6 +52,8 @@ def lib():
         L.ro_scene_num_triangles.argtypes = [C.c_void_p]
         L.ro_scene_camera.argtypes = [C.c_void_p, fp]
         L.ro_scene_set_camera.argtypes = [C.c_void_p, fp]
+        L.ro_scene_set_material.restype = C.c_int
+        L.ro_scene_set_material.argtypes = [C.c_void_p, C.c_int, C.c_size_t, fp]
         L.ro_scene_sphere.argtypes = [C.c_void_p, C.c_size_t, fp]
         L.ro_scene_triangle.argtypes = [C.c_void_p, C.c_size_t, fp]
         L.ro_camera_new_at.argtypes = [fp, C.c_float, fp]
@@ -124,6 +126,11 @@ class Scene:
         c = np.zeros(12, np.float32)
         lib().ro_scene_camera(self._h, fptr(c))
         return c
+
+    def set_material(self, i, kind, rgb, param=0.0, triangle=False):
+        m = np.array([kind, rgb[0], rgb[1], rgb[2], 1.0, param], np.float32)
+        if lib().ro_scene_set_material(self._h, 1 if triangle else 0, i, fptr(m)) != 0:
+            raise IndexError(i)
 
     def set_camera(self, cam):
         c = f32arr(cam)

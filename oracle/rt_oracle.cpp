@@ -620,6 +620,20 @@ static Material mat_in(const float o[6]) {
     m.type = (int)o[0]; m.color = C4{o[1], o[2], o[3], o[4]}; m.param = o[5];
     return m;
 }
+
+// Test hook: replaces one primitive's material (each owns a copy, as
+// parser.rs:237-310 clone the named material), e.g. with Emission
+// (materials.rs:100-102), which the grammar cannot produce.
+int ro_scene_set_material(ro_scene *s, int triangle, size_t i, const float m[6]) {
+    if (triangle) {
+        if (i >= s->world.triangles.size()) return -1;
+        s->world.triangles[i].mat = mat_in(m);
+    } else {
+        if (i >= s->world.spheres.size()) return -1;
+        s->world.spheres[i].mat = mat_in(m);
+    }
+    return 0;
+}
 void ro_scene_sphere(const ro_scene *s, size_t i, float out[10]) {
     const Sphere &sp = s->world.spheres[i];
     out[0] = sp.center.x; out[1] = sp.center.y; out[2] = sp.center.z; out[3] = sp.radius;

@@ -48,6 +48,8 @@ size_t ro_scene_num_triangles(const ro_scene *s);
 /* camera[12] = origin, lower_left_corner, horizontal, vertical (camera.rs:8-15) */
 void ro_scene_camera(const ro_scene *s, float camera[12]);
 void ro_scene_set_camera(ro_scene *s, const float camera[12]);
+/* replaces sphere (triangle != 0: triangle) i's material (type r g b a param) */
+int ro_scene_set_material(ro_scene *s, int triangle, size_t i, const float m[6]);
 /* sphere i: center(3) radius(1) material(6) = type, r, g, b, a, param */
 void ro_scene_sphere(const ro_scene *s, size_t i, float out[10]);
 /* triangle i: v0 v1 v2 (9) normal(3) material(6) */

@@ -510,7 +510,11 @@ SphereBVH build_sphere_bvh(const std::vector<Sphere> &spheres, uint32_t leaf_siz
     // spheres above big_k x the median radius stay out of the tree (A/B on C2:
     // 4 -> 5.41 ms, 8 -> 5.35, 16 -> 5.34; the ground sphere in the tree -> 97)
     double big_k = 8.0;
-    if (const char *e = std::getenv("RT_AMD_BIG_K")) big_k = std::atof(e);
+    if (const char *e = std::getenv("RT_AMD_BIG_K")) {
+        // a typo (0), a negative or non-finite value keeps the default
+        const double k = std::atof(e);
+        if (std::isfinite(k) && k > 0.0) big_k = k;
+    }
     for (uint32_t i = 0; i < spheres.size(); ++i) {
         const Sphere &s = spheres[i];
         const double r = std::fabs((double)s.radius);

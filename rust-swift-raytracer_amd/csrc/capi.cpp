@@ -30,6 +30,16 @@ RtRenderOptions reference_options() {
     rt_default_options(&o);
     return o;
 }
+
+// render()'s device count: RT_AMD_DEVICES=N (N >= 1) row-tiles its frames over
+// N devices; unset, invalid or 0 keeps one device
+int32_t env_devices() {
+    const char *e = std::getenv("RT_AMD_DEVICES");
+    if (!e || !*e) return 0;
+    char *end = nullptr;
+    const long n = std::strtol(e, &end, 10);
+    return (end && *end == '\0' && n >= 1 && n <= 64) ? (int32_t)n : 0;
+}
 }  // namespace
 
 extern "C" {
@@ -77,6 +87,7 @@ Rust_Camera *move_camera_position(Rust_Camera *camera, float x, float y, float z
 // caller's pixels (the reference returned a pointer into a freed Vec).
 Rust_CFramebuffer render(Rust_CFramebuffer framebuffer, const Rust_WorldHandle *handle) {
     RtRenderOptions o = reference_options();
+    o.ndevices = env_devices();
     int rc = rt_render_ex(framebuffer, handle, &o, nullptr);
     if (rc != 0) {
         std::fprintf(stderr, "raytracer render() failed (%d): %s\n", rc, rtamd::last_error().c_str());
@@ -91,7 +102,7 @@ void rt_default_options(RtRenderOptions *o) {
     o->max_ray_bounces = 8;     // lib.rs:51
     o->rng_mode = RT_RNG_COUNTER;
     o->seed = 2547549u;         // random.rs:9
-    o->row_block = 1;
+    o->row_block = 8;  // multi-GPU tiles: blocks of 8 rows
     o->rank = 0;
     o->nranks = 1;
     o->device = -1;
@@ -135,6 +146,10 @@ int rt_render_device(const Rust_WorldHandle *h, size_t width, size_t height,
         return -1;
     }
     RtRenderOptions o = opts ? *opts : reference_options();
+    if (o.ndevices >= 1)
+        return rtamd::render_frame_multi(h->world->state, h->camera->cam, width, height, o,
+                                         static_cast<uint32_t *>(d_rgba),
+                                         static_cast<hipStream_t>(hip_stream), stats);
     return rtamd::render_frame(h->world->state, h->camera->cam, width, height, o,
                                static_cast<uint32_t *>(d_rgba),
                                static_cast<hipStream_t>(hip_stream), stats);
@@ -164,6 +179,39 @@ size_t rt_world_num_spheres(const Rust_WorldHandle *h) {
 }
 size_t rt_world_num_triangles(const Rust_WorldHandle *h) {
     return h && h->world ? h->world->state.scene.triangles.size() : 0;
+}
+
+// Replaces primitive i's material.  Each primitive owns its material copy
+// (parser.rs:237-310 clone the named material), so this changes one primitive.
+static int set_material(Rust_WorldHandle *h, bool tri, size_t i, const float *m) {
+    if (!h || !h->world || !m) return -1;
+    rtamd::WorldState &w = h->world->state;
+    std::lock_guard<std::recursive_mutex> lock(w.mu);
+    rtamd::SceneModel &sc = w.scene;
+    if (tri ? i >= sc.triangles.size() : i >= sc.spheres.size()) {
+        rtamd::set_error("set material: primitive index out of range");
+        return -1;
+    }
+    // kinds of materials.rs:7-12; every Color the reference builds has alpha 1.0
+    // (color.rs:21-23), which the resolve relies on
+    const float k = m[0];
+    if (!(k == 0.0f || k == 1.0f || k == 2.0f || k == 3.0f) || m[4] != 1.0f) {
+        rtamd::set_error("set material: kind must be 0-3 and alpha 1.0");
+        return -1;
+    }
+    const uint32_t idx = tri ? sc.triangles[i].material : sc.spheres[i].material;
+    sc.materials[idx] = rtamd::Material{(uint32_t)k, m[1], m[2], m[3], m[4], m[5]};
+    w.packed = rtamd::pack_scene(sc, 8, 1);
+    w.devices.clear();  // the next frame uploads the scene again
+    return 0;
+}
+
+int rt_world_set_sphere_material(Rust_WorldHandle *h, size_t i, const float material[6]) {
+    return set_material(h, false, i, material);
+}
+
+int rt_world_set_triangle_material(Rust_WorldHandle *h, size_t i, const float material[6]) {
+    return set_material(h, true, i, material);
 }
 
 static void material_out(const rtamd::Material &m, float *o) {
@@ -206,6 +254,8 @@ int rt_write_ppm(const Rust_CFramebuffer *fb, const char *path) {
     }
     return std::fclose(f) == 0 ? 0 : -1;
 }
+
+int rt_comm_count(int first, int n) { return rtamd::comm_count(first, n); }
 
 int rt_device_count(void) {
     int n = 0;

@@ -101,6 +101,12 @@ hipError_t launch_trace(const TraceParams &p, uint32_t blocks, hipStream_t strea
 hipError_t launch_resolve_ex(const float *samples, uint32_t *out, uint32_t npix, uint32_t spp,
                              float inv_spp, uint32_t width, uint32_t slab_row0,
                              hipStream_t stream);
+// Reassembles a gathered multi-device frame: gathered holds nranks tiles of
+// max_rows rows (row-cyclic blocks of row_block rows), out the width x height
+// frame (top row first).
+hipError_t launch_assemble(const uint32_t *gathered, uint32_t *out, uint32_t width, uint32_t height,
+                           uint32_t row_block, uint32_t nranks, uint32_t max_rows,
+                           hipStream_t stream);
 // variant: 0 brute force, 1 BVH from global memory, 2 BVH staged in LDS;
 // step: the sliced-walk kernel (TraceParams::step); tri: the scene has triangles
 // workgroups per CU of one trace_kernel instance (count: the counting variant)

@@ -1285,4 +1285,35 @@ hipError_t trace_occupancy(int *blocks_per_cu, int variant, size_t lds_bytes, bo
                  : trace_occupancy_c<false>(blocks_per_cu, variant, lds_bytes, step, tri);
 }
 
+// Multi-device frames (runtime.cpp render_frame_multi): rank g's tile holds
+// the image rows of its row blocks (tile row k = image row tile_row(k)); the
+// root's gather buffer holds nranks tiles of max_rows rows each.  One thread
+// per RGBA8 word of the frame reads its word from its rank's tile: the frame
+// is written once, coalesced, and the gathered tiles are read once.
+__global__ __launch_bounds__(256) void assemble_kernel(const uint32_t *__restrict__ gathered,
+                                                       uint32_t *__restrict__ out, uint32_t width,
+                                                       uint32_t height, uint32_t row_block,
+                                                       uint32_t nranks, uint32_t max_rows) {
+    const uint64_t n = (uint64_t)width * height;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t row = (uint32_t)(i / width), col = (uint32_t)(i - (uint64_t)row * width);
+        const uint32_t b = row / row_block;
+        const uint32_t g = b % nranks;
+        const uint32_t k = (b / nranks) * row_block + row % row_block;
+        out[i] = gathered[((uint64_t)g * max_rows + k) * width + col];
+    }
+}
+
+hipError_t launch_assemble(const uint32_t *gathered, uint32_t *out, uint32_t width, uint32_t height,
+                           uint32_t row_block, uint32_t nranks, uint32_t max_rows,
+                           hipStream_t stream) {
+    const uint64_t n = (uint64_t)width * height;
+    if (!n) return hipSuccess;
+    const uint64_t want = (n + 255) / 256, blocks = want < 256 * 64 ? want : 256 * 64;
+    hipLaunchKernelGGL(assemble_kernel, dim3((uint32_t)blocks), dim3(256), 0, stream, gathered, out,
+                       width, height, row_block ? row_block : 1, nranks ? nranks : 1, max_rows);
+    return hipGetLastError();
+}
+
 }  // namespace rtamd

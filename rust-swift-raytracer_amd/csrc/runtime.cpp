@@ -14,6 +14,9 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <vector>
+
+#include <rccl/rccl.h>
 
 #include "../../include/raytracer_amd.h"
 #include "render.h"
@@ -48,11 +51,12 @@ DeviceState::~DeviceState() {
     void *bufs[] = {sph_hot, sph_cold, tri_hot, tri_geo, mats, samples, ring, out, replay, counter, stats,
                     bvh_nodes, bvh_prims, big_hot, bvh_miss, bvh_prim_id, big_id, bvh_miss16,
                     sph_shade, sph_kind, tbvh_nodes, tbvh_tris, tbvh_loose,
-                    cam_nodes, cam_tris, ptl_off, ptl_items, spl};
+                    cam_nodes, cam_tris, ptl_off, ptl_items, spl, tile, gath};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
     for (hipEvent_t e : ev)
         if (e) (void)hipEventDestroy(e);
+    if (done) (void)hipEventDestroy(done);
     if (stream) (void)hipStreamDestroy(stream);
 }
 
@@ -93,6 +97,7 @@ static int device_for(WorldState &w, int want, DeviceState *&out) {
         d->device = dev;
         HIP_TRY(hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking));
         for (auto &e : d->ev) HIP_TRY(hipEventCreate(&e));
+        HIP_TRY(hipEventCreateWithFlags(&d->done, hipEventDisableTiming));
         hipDeviceProp_t prop;
         HIP_TRY(hipGetDeviceProperties(&prop, dev));
         d->num_cus = prop.multiProcessorCount;
@@ -255,10 +260,14 @@ int render_frame(WorldState &w, const CameraModel &cam, size_t width, size_t hei
     if (width == 0 || T == 0) return 0;
     if (!d_out) { set_error("null output"); return -1; }
 
+    std::lock_guard<std::recursive_mutex> lock(w.mu);
     DeviceState *d = nullptr;
     int rc = device_for(w, o.device, d);
     if (rc) return rc;
     hipStream_t s = stream ? stream : d->stream;
+    // the device's scratch (job counters, rings, slab, stats) is shared by every
+    // frame on it: a frame enqueued on another stream waits for the last one
+    if (d->done_stream && d->done_stream != s) HIP_TRY(hipStreamWaitEvent(s, d->done, 0));
 
     const uint32_t spp = o.samples_per_pixel > 0 ? (uint32_t)o.samples_per_pixel : 0u;
     const uint64_t jobs_per_row = (uint64_t)width * spp;
@@ -514,6 +523,8 @@ int render_frame(WorldState &w, const CameraModel &cam, size_t width, size_t hei
             resolve_ms += b;
         }
     }
+    HIP_TRY(hipEventRecord(d->done, s));
+    d->done_stream = s;
     // without stats the frame stays asynchronous on the stream (no host wait)
     if (!timed) return 0;
     std::vector<unsigned long long> rec(max_waves * kStatSlots);
@@ -573,8 +584,171 @@ long read_samples(WorldState &w, int device, float *out, size_t n) {
     return (long)(count * 4);
 }
 
+#define NCCL_TRY(expr)                                                                \
+    do {                                                                              \
+        ncclResult_t r_ = (expr);                                                     \
+        if (r_ != ncclSuccess) {                                                      \
+            set_error(std::string(#expr) + " failed: " + ncclGetErrorString(r_));     \
+            return -4;                                                                \
+        }                                                                             \
+    } while (0)
+
+namespace {
+// RCCL communicators, one set per device list (ncclCommInitAll is expensive:
+// created once per process and kept; map nodes are stable)
+std::mutex g_comm_mu;
+std::map<std::vector<int>, std::vector<ncclComm_t>> g_comms;
+
+int device_comms(const std::vector<int> &devs, std::vector<ncclComm_t> *&out) {
+    std::lock_guard<std::mutex> lock(g_comm_mu);
+    auto it = g_comms.find(devs);
+    if (it == g_comms.end()) {
+        std::vector<ncclComm_t> c(devs.size(), nullptr);
+        NCCL_TRY(ncclCommInitAll(c.data(), (int)devs.size(), devs.data()));
+        it = g_comms.emplace(devs, std::move(c)).first;
+    }
+    out = &it->second;
+    return 0;
+}
+
+int device_list(int first, int n, std::vector<int> &devs) {
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) {
+        set_error("no HIP device available: the MI355X render path requires a GPU");
+        return -3;
+    }
+    if (first < 0) HIP_TRY(hipGetDevice(&first));
+    if (n < 1 || first + n > count) {
+        set_error("ndevices: devices [" + std::to_string(first) + ", " + std::to_string(first + n) +
+                  ") are not all visible (" + std::to_string(count) + " devices)");
+        return -1;
+    }
+    devs.resize(n);
+    for (int g = 0; g < n; ++g) devs[g] = first + g;
+    return 0;
+}
+}  // namespace
+
+int comm_count(int first, int n) {
+    std::vector<int> devs;
+    int rc = device_list(first, n, devs);
+    if (rc) return rc;
+    std::vector<ncclComm_t> *comms = nullptr;
+    rc = device_comms(devs, comms);
+    if (rc) return rc;
+    int ranks = 0;
+    NCCL_TRY(ncclCommCount((*comms)[0], &ranks));
+    return ranks;
+}
+
+int render_frame_multi(WorldState &w, const CameraModel &cam, size_t width, size_t height,
+                       const RtRenderOptions &o, uint32_t *d_out, hipStream_t stream,
+                       RtRenderStats *stats) {
+    if (stats) std::memset(stats, 0, sizeof(*stats));
+    if ((o.nranks > 1) || o.rank) {
+        set_error("ndevices renders the whole frame: rank/nranks must be 0/1");
+        return -1;
+    }
+    std::lock_guard<std::recursive_mutex> lock(w.mu);
+    std::vector<int> devs;
+    int rc = device_list(o.device, o.ndevices, devs);
+    if (rc) return rc;
+    const uint32_t n = (uint32_t)devs.size();
+    const uint32_t B = o.row_block ? o.row_block : 8;
+    if (width == 0 || height == 0) return 0;
+    if (!d_out) { set_error("null output"); return -1; }
+    if (width > 0xFFFFFFu || height > 0xFFFFFFu) { set_error("frame too large"); return -1; }
+    size_t max_rows = 0;
+    for (uint32_t g = 0; g < n; ++g) max_rows = std::max(max_rows, tile_rows(height, B, g, n));
+    std::vector<ncclComm_t> *comms = nullptr;
+    rc = device_comms(devs, comms);
+    if (rc) return rc;
+    std::vector<DeviceState *> ds(n, nullptr);
+    std::vector<hipStream_t> ss(n, nullptr);
+    for (uint32_t g = 0; g < n; ++g) {
+        rc = device_for(w, devs[g], ds[g]);
+        if (rc) return rc;
+        ss[g] = (g == 0 && stream) ? stream : ds[g]->stream;
+        HIP_TRY(grow(ds[g]->tile, ds[g]->tile_cap, max_rows * width));
+    }
+    if (n > 1) {
+        HIP_TRY(hipSetDevice(devs[0]));
+        HIP_TRY(grow(ds[0]->gath, ds[0]->gath_cap, n * max_rows * width));
+    }
+    // every device renders its row blocks (asynchronously unless stats are
+    // wanted: counters need a host wait per device)
+    for (uint32_t g = 0; g < n; ++g) {
+        RtRenderOptions og = o;
+        og.ndevices = 0;
+        og.rank = g;
+        og.nranks = n;
+        og.row_block = B;
+        og.device = devs[g];
+        RtRenderStats sg;
+        rc = render_frame(w, cam, width, height, og, ds[g]->tile, ss[g], stats ? &sg : nullptr);
+        if (rc) return rc;
+        if (stats) {
+            stats->samples += sg.samples; stats->rays += sg.rays;
+            stats->sphere_tests += sg.sphere_tests; stats->tri_tests += sg.tri_tests;
+            stats->tri_in_range += sg.tri_in_range;
+            stats->trace_ms = std::max(stats->trace_ms, sg.trace_ms);
+            stats->resolve_ms = std::max(stats->resolve_ms, sg.resolve_ms);
+            stats->trace_launches = std::max(stats->trace_launches, sg.trace_launches);
+            stats->waves += sg.waves; stats->accel = sg.accel;
+            stats->bvh_sphere_tests += sg.bvh_sphere_tests; stats->bvh_node_tests += sg.bvh_node_tests;
+            stats->big_sphere_tests += sg.big_sphere_tests;
+            for (int k = 0; k < 4; ++k) stats->stamp_cycles[k] += sg.stamp_cycles[k];
+            stats->tri_node_tests += sg.tri_node_tests; stats->bvh_tri_tests += sg.bvh_tri_tests;
+            stats->tri_bvh = sg.tri_bvh; stats->fused_resolve = sg.fused_resolve;
+        }
+    }
+    // RCCL gather of equal-size tiles to the first device (over xGMI); with one
+    // device the tile is the frame and the gather lands in d_out directly
+    const size_t bytes = max_rows * width * 4;
+    NCCL_TRY(ncclGroupStart());
+    for (uint32_t g = 0; g < n; ++g)
+        NCCL_TRY(ncclGather(ds[g]->tile, n > 1 ? (void *)ds[0]->gath : (void *)d_out, bytes, ncclUint8,
+                            0, (*comms)[g], ss[g]));
+    NCCL_TRY(ncclGroupEnd());
+    HIP_TRY(hipSetDevice(devs[0]));
+    if (n > 1)
+        HIP_TRY(launch_assemble(ds[0]->gath, d_out, (uint32_t)width, (uint32_t)height, B, n,
+                                (uint32_t)max_rows, ss[0]));
+    // the tiles and the gather buffer are reused by the next frame on these streams
+    for (uint32_t g = 0; g < n; ++g) {
+        HIP_TRY(hipSetDevice(devs[g]));
+        HIP_TRY(hipEventRecord(ds[g]->done, ss[g]));
+        ds[g]->done_stream = ss[g];
+    }
+    HIP_TRY(hipSetDevice(devs[0]));
+    if (stats) HIP_TRY(hipStreamSynchronize(ss[0]));
+    return 0;
+}
+
 int render_frame_host(WorldState &w, const CameraModel &cam, size_t width, size_t height,
                       const RtRenderOptions &o, void *host_out, RtRenderStats *stats) {
+    std::lock_guard<std::recursive_mutex> lock(w.mu);
+    if (o.ndevices >= 1) {
+        if (width == 0 || height == 0) {
+            if (stats) std::memset(stats, 0, sizeof(*stats));
+            return 0;
+        }
+        if (!host_out) { set_error("null framebuffer pixels"); return -1; }
+        std::vector<int> devs;
+        int rc = device_list(o.device, o.ndevices, devs);
+        if (rc) return rc;
+        DeviceState *root = nullptr;
+        rc = device_for(w, devs[0], root);
+        if (rc) return rc;
+        HIP_TRY(grow(root->out, root->out_cap, width * height));
+        rc = render_frame_multi(w, cam, width, height, o, root->out, root->stream, stats);
+        if (rc) return rc;
+        HIP_TRY(hipSetDevice(devs[0]));
+        HIP_TRY(hipMemcpyAsync(host_out, root->out, width * height * 4, hipMemcpyDeviceToHost,
+                               root->stream));
+        HIP_TRY(hipStreamSynchronize(root->stream));
+        return 0;
+    }
     const uint32_t nranks = o.nranks ? o.nranks : 1;
     const uint32_t B = nranks > 1 ? (o.row_block ? o.row_block : 1) : (uint32_t)std::max<size_t>(height, 1);
     const size_t T = o.rank < nranks ? tile_rows(height, B, o.rank, nranks) : 0;

@@ -5,6 +5,7 @@
 
 #include <cstdint>
 #include <map>
+#include <mutex>
 #include <memory>
 #include <string>
 
@@ -51,6 +52,10 @@ struct DeviceState {
     float *samples = nullptr;        size_t samples_cap = 0;   // sample slab (3 planes)
     float *ring = nullptr;           size_t ring_cap = 0;      // per-wave sample rings (fused resolve)
     uint32_t *out = nullptr;         size_t out_cap = 0;       // RGBA8 tile (host path)
+    uint32_t *tile = nullptr;        size_t tile_cap = 0;      // multi-device: this rank's tile
+    uint32_t *gath = nullptr;        size_t gath_cap = 0;      // multi-device root: gathered tiles
+    hipEvent_t done = nullptr;       // end of the last frame enqueued on this device ...
+    hipStream_t done_stream = nullptr;  // ... and the stream it was enqueued on
     uint32_t *replay = nullptr;      size_t replay_cap = 0;
     uint32_t *counter = nullptr;                                // job counter
     unsigned long long *stats = nullptr; size_t stats_cap = 0;  // per-wave counter records
@@ -80,6 +85,9 @@ struct WorldState {
     size_t spl_w = 0, spl_h = 0;
     uint64_t spl_version = 0;
     std::map<int, std::unique_ptr<DeviceState>> devices;
+    // one frame at a time per handle: calls from several host threads are
+    // serialised here (render_frame_multi re-enters render_frame)
+    std::recursive_mutex mu;
 };
 
 // Renders rank's tile of a width x height frame into device memory d_out
@@ -87,6 +95,21 @@ struct WorldState {
 int render_frame(WorldState &w, const CameraModel &cam, size_t width, size_t height,
                  const RtRenderOptions &opts, uint32_t *d_out, hipStream_t stream,
                  RtRenderStats *stats);
+
+// A frame row-tiled over opts.ndevices devices (first = opts.device, or the
+// current device) in this one process: each device renders its row blocks
+// (blocks of opts.row_block rows, round-robin) into its own tile, an RCCL
+// ncclGather (communicators from ncclCommInitAll, cached per device list)
+// collects the tiles on the first device, and assemble_kernel writes the
+// frame to d_out there (width x height RGBA8, top row first).  stream (may be
+// null) is a stream of the first device; the others use their library streams.
+int render_frame_multi(WorldState &w, const CameraModel &cam, size_t width, size_t height,
+                       const RtRenderOptions &opts, uint32_t *d_out, hipStream_t stream,
+                       RtRenderStats *stats);
+
+// Ranks of the cached RCCL communicator of devices [first, first + n)
+// (created on first use), or a negative error.
+int comm_count(int first, int n);
 
 // Same, into host memory (the reference's synchronous render(), lib.rs:49-57).
 int render_frame_host(WorldState &w, const CameraModel &cam, size_t width, size_t height,

@@ -28,7 +28,8 @@ EXPORTS = (
     "rt_default_options", "rt_tile_rows", "rt_tile_row", "rt_sample_seed", "rt_render_ex",
     "rt_render_device", "rt_read_samples", "rt_free_world", "rt_last_error", "rt_world_num_spheres",
     "rt_world_num_triangles", "rt_world_sphere", "rt_world_triangle", "rt_camera_get",
-    "rt_last_parse_error", "rt_write_ppm", "rt_device_count",
+    "rt_last_parse_error", "rt_write_ppm", "rt_device_count", "rt_comm_count",
+    "rt_world_set_sphere_material", "rt_world_set_triangle_material",
 )
 
 
@@ -53,7 +54,7 @@ class RenderOptions(C.Structure):
                 ("rng_mode", C.c_uint32), ("seed", C.c_uint32),
                 ("replay_states", C.POINTER(C.c_uint32)), ("row_block", C.c_uint32),
                 ("rank", C.c_uint32), ("nranks", C.c_uint32), ("device", C.c_int32),
-                ("accel", C.c_int32), ("flags", C.c_uint32)]
+                ("accel", C.c_int32), ("flags", C.c_uint32), ("ndevices", C.c_int32)]
 
 
 class RenderStats(C.Structure):
@@ -122,10 +123,15 @@ def lib(path=None):
         L.rt_world_triangle.restype = C.c_int
         L.rt_world_triangle.argtypes = [H, C.c_size_t, fp]
         L.rt_camera_get.argtypes = [C.c_void_p, fp]
+        for f in (L.rt_world_set_sphere_material, L.rt_world_set_triangle_material):
+            f.restype = C.c_int
+            f.argtypes = [H, C.c_size_t, fp]
         L.rt_last_parse_error.restype = C.c_int
         L.rt_write_ppm.restype = C.c_int
         L.rt_write_ppm.argtypes = [C.POINTER(CFramebuffer), C.c_char_p]
         L.rt_device_count.restype = C.c_int
+        L.rt_comm_count.restype = C.c_int
+        L.rt_comm_count.argtypes = [C.c_int, C.c_int]
         _libs[path] = L
     return _libs[path]
 
@@ -136,6 +142,15 @@ def last_error() -> str:
 
 def device_count() -> int:
     return int(lib().rt_device_count())
+
+
+def comm_count(first: int, n: int) -> int:
+    """Ranks of the RCCL communicator a multi-device frame over devices
+    [first, first + n) uses (created on first use); raises on error."""
+    r = int(lib().rt_comm_count(first, n))
+    if r < 0:
+        raise RenderError(f"rt_comm_count failed ({r}): {last_error()}")
+    return r
 
 
 def tile_rows(height, row_block, rank, nranks) -> int:
@@ -150,13 +165,15 @@ def sample_seed(seed: int, job: int) -> int:
     return int(lib().rt_sample_seed(seed, job))
 
 
-def options(spp=16, depth=8, mode=RNG_COUNTER, seed=DEFAULT_SEED, replay=None, row_block=1,
-            rank=0, nranks=1, device=-1, accel=ACCEL_AUTO, keep_samples=False, L=None):
+def options(spp=16, depth=8, mode=RNG_COUNTER, seed=DEFAULT_SEED, replay=None, row_block=8,
+            rank=0, nranks=1, device=-1, accel=ACCEL_AUTO, keep_samples=False, L=None,
+            ndevices=0):
     o = RenderOptions()
     (L or lib()).rt_default_options(C.byref(o))
     o.samples_per_pixel, o.max_ray_bounces, o.rng_mode, o.seed = spp, depth, mode, seed
     o.row_block, o.rank, o.nranks, o.device = row_block, rank, nranks, device
     o.accel = accel
+    o.ndevices = ndevices
     o.flags = FLAG_KEEP_SAMPLES if keep_samples else 0
     keep = None
     if replay is not None:
@@ -211,6 +228,14 @@ class World:
             self._L.rt_world_triangle(self._h, i, out[i].ctypes.data_as(C.POINTER(C.c_float)))
         return out
 
+    def set_material(self, i, kind, rgb, param=0.0, triangle=False):
+        """rt_world_set_{sphere,triangle}_material: kind 0 Diffuse, 1 Metal,
+        2 Dielectric, 3 Emission (materials.rs:7-12)."""
+        m = np.array([kind, rgb[0], rgb[1], rgb[2], 1.0, param], np.float32)
+        f = self._L.rt_world_set_triangle_material if triangle else self._L.rt_world_set_sphere_material
+        if f(self._h, i, m.ctypes.data_as(C.POINTER(C.c_float))) != 0:
+            raise ValueError(f"set_material failed: {last_error()}")
+
     def camera(self):
         c = np.zeros(12, np.float32)
         self._L.rt_camera_get(self._h.contents.camera, c.ctypes.data_as(C.POINTER(C.c_float)))
@@ -230,14 +255,16 @@ class World:
         return px
 
     def render(self, width, height, spp=16, depth=8, mode=RNG_COUNTER, seed=DEFAULT_SEED,
-               replay=None, row_block=1, rank=0, nranks=1, device=-1, accel=ACCEL_AUTO,
-               keep_samples=False, stats=True):
+               replay=None, row_block=8, rank=0, nranks=1, device=-1, accel=ACCEL_AUTO,
+               keep_samples=False, stats=True, ndevices=0):
         """rt_render_ex -> (rgba uint8[tile_rows, width, 4], stats dict).
         keep_samples: write every sample to the slab (for read_samples) and
         resolve with the second kernel; the frame is bit-identical.
-        stats=False: no counters (the kernel variant without them; stats None)."""
+        stats=False: no counters (the kernel variant without them; stats None).
+        ndevices >= 1: the whole frame, row-tiled over that many devices of this
+        process and gathered with RCCL (RtRenderOptions.ndevices)."""
         o, keep = options(spp, depth, mode, seed, replay, row_block, rank, nranks, device, accel,
-                          keep_samples, self._L)
+                          keep_samples, self._L, ndevices)
         rows = int(self._L.rt_tile_rows(height, row_block, rank, nranks)) if nranks > 1 else height
         px = np.zeros((rows, width, 4), np.uint8)
         fb = CFramebuffer(width, height, px.ctypes.data_as(C.POINTER(ColorU8)))
@@ -258,13 +285,13 @@ class World:
         return out[: n // 4]
 
     def render_device(self, width, height, out_ptr: int, stream_ptr: int = 0, spp=16, depth=8,
-                      mode=RNG_COUNTER, seed=DEFAULT_SEED, row_block=1, rank=0, nranks=1,
-                      device=-1, accel=ACCEL_AUTO, stats=True, keep_samples=False):
+                      mode=RNG_COUNTER, seed=DEFAULT_SEED, row_block=8, rank=0, nranks=1,
+                      device=-1, accel=ACCEL_AUTO, stats=True, keep_samples=False, ndevices=0):
         """rt_render_device into a device buffer (e.g. a torch uint8 tensor).
         stats=False: no counters and no host wait -- the frame is only enqueued
         on the stream (returns None)."""
         o, _ = options(spp, depth, mode, seed, None, row_block, rank, nranks, device, accel,
-                       keep_samples, self._L)
+                       keep_samples, self._L, ndevices)
         st = RenderStats()
         rc = self._L.rt_render_device(self._h, width, height, C.byref(o), C.c_void_p(out_ptr),
                                     C.c_void_p(stream_ptr or None), C.byref(st) if stats else None)

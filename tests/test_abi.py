@@ -64,11 +64,21 @@ _Static_assert(offsetof(Rust_CFramebuffer, pixels) == 16, "CFramebuffer.pixels")
 _Static_assert(sizeof(Rust_WorldHandle) == 16, "WorldHandle");
 _Static_assert(offsetof(Rust_WorldHandle, camera) == 8, "WorldHandle.camera");
 _Static_assert(sizeof(Rust_NVec3) == 12, "NVec3");
-int main(void) { Rust_NVec3 x = Rust_X_AXIS; return (int)x.y; }
+#include <stdio.h>
+int main(void) {
+  printf("%zu %zu %zu %zu\n", sizeof(RtRenderOptions), offsetof(RtRenderOptions, ndevices),
+         sizeof(RtRenderStats), offsetof(RtRenderStats, fused_resolve));
+  return 0;
+}
 """)
     subprocess.run(["gcc", "-std=c11", "-Wall", "-Werror", f"-I{INC}", "-o",
                     str(tmp_path / "layout"), str(src)], check=True)
     assert C.sizeof(R.CFramebuffer) == 24 and C.sizeof(R.WorldHandle) == 16
+    # the ctypes mirrors of the extension structs match the C layouts
+    got = subprocess.run([str(tmp_path / "layout")], capture_output=True, text=True,
+                         check=True).stdout.split()
+    assert [int(x) for x in got] == [C.sizeof(R.RenderOptions), R.RenderOptions.ndevices.offset,
+                                     C.sizeof(R.RenderStats), R.RenderStats.fused_resolve.offset]
 
 
 def test_c_example_links_against_the_header():
@@ -83,6 +93,7 @@ def test_default_options_are_the_reference_hard_codes():
     o, _ = R.options()
     assert (o.samples_per_pixel, o.max_ray_bounces) == (16, 8)  # lib.rs:51
     assert o.seed == 2547549 and o.rng_mode == R.RNG_COUNTER and o.nranks == 1
+    assert o.ndevices == 0 and o.row_block == 8  # one device unless asked
 
 
 def test_counter_seed_spec_matches_oracle():
@@ -108,6 +119,16 @@ def test_render_fails_loudly_without_gpu():
     fb = R.CFramebuffer(8, 8, px.ctypes.data_as(C.POINTER(R.ColorU8)))
     res = R.lib().render(fb, w.handle)
     assert not res.pixels and res.width == 0
+
+
+@pytest.mark.skipif(R.device_count() > 0, reason="a GPU is present")
+def test_multi_device_mode_fails_loudly_without_gpu():
+    w = R.World(scene_text("world.txt"))
+    for n in (1, 2, 8):
+        with pytest.raises(R.RenderError, match="no HIP device"):
+            w.render(8, 8, ndevices=n)
+        with pytest.raises(R.RenderError, match="no HIP device"):
+            R.comm_count(0, n)
 
 
 def test_load_world_null_and_free():

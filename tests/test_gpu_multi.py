@@ -1,0 +1,121 @@
+"""GPU tests of the multi-GPU paths.
+
+The reference renders serially (common.rs:327-358); the north star row-tiles
+the frame over the node's GPUs and gathers the tiles over RCCL.  Two launch
+shapes exist and both are exercised here on the one GPU a test box has:
+  * one process, N devices (RtRenderOptions.ndevices): tiles + RCCL ncclGather
+    (ncclCommInitAll communicator) + assemble kernel, through the C-ABI.  With
+    one device the gather is a copy into the frame.  Bit-identical to the
+    single-device frame, through rt_render_ex, rt_render_device and render()
+    (RT_AMD_DEVICES);
+  * one process per GPU (torch.distributed.run, the driver's N>1 launch):
+    rehearsed with two ranks sharing device 0 and gloo collectives, HIP tiles,
+    the gathered frame checked against a one-rank render (RT_BENCH_VERIFY).
+Plus `python bench.py --gpus 1`, which runs the single-process path.
+"""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+import oracle as O
+import raytracer_amd as R
+from conftest import ROOT, scene_text
+from test_gpu_parity import assert_bits_equal
+
+pytestmark = pytest.mark.gpu
+
+
+def test_comm_count_one_device():
+    assert R.comm_count(0, 1) == 1
+    with pytest.raises(R.RenderError, match="not all visible"):
+        R.comm_count(0, R.device_count() + 1)
+
+
+@pytest.mark.parametrize("scene,w,h,spp", [("rtow.txt", 160, 90, 4), ("c_raytracer_world.txt", 61, 37, 3)])
+def test_ndevices_one_equals_single_device(scene, w, h, spp):
+    world = R.World(scene_text(scene))
+    ref, st = world.render(w, h, spp, 8)
+    out, st1 = world.render(w, h, spp, 8, ndevices=1)
+    assert_bits_equal(out, ref, "ndevices=1 frame")
+    assert st1["rays"] == st["rays"] and st1["samples"] == st["samples"]
+    lean, _ = world.render(w, h, spp, 8, ndevices=1, stats=False)
+    assert_bits_equal(lean, ref, "ndevices=1 frame without counters")
+    with pytest.raises(R.RenderError, match="rank/nranks"):
+        world.render(w, h, spp, 8, ndevices=1, rank=1, nranks=2)
+    with pytest.raises(R.RenderError, match="not all visible"):
+        world.render(w, h, spp, 8, ndevices=R.device_count() + 1)
+
+
+def test_ndevices_render_device_into_torch_frame():
+    import torch
+
+    world = R.World(scene_text("rtow.txt"))
+    w, h, spp = 96, 54, 4
+    ref, _ = world.render(w, h, spp, 8)
+    frame = torch.zeros(h * w * 4, dtype=torch.uint8, device="cuda:0")
+    stream = torch.cuda.Stream(device="cuda:0")
+    for _ in range(3):  # frames pipelined on the caller's stream, no host wait
+        world.render_device(w, h, frame.data_ptr(), stream.cuda_stream, spp=spp, depth=8,
+                            device=0, stats=False, ndevices=1)
+    torch.cuda.synchronize(0)
+    assert_bits_equal(frame.cpu().numpy().reshape(h, w, 4), ref, "device frame")
+
+
+def test_render_entry_point_with_rt_amd_devices(monkeypatch):
+    """render() (lib.rs:49-57, 16 spp / depth 8) spread over RT_AMD_DEVICES."""
+    src = scene_text("c_raytracer_world.txt")
+    img, _, _ = O.Scene(src).render(40, 30, 16, 8, mode=O.RNG_COUNTER, nthreads=8)
+    world = R.World(src)
+    for v in ("1", "0", "junk"):  # 0 / invalid: one device
+        monkeypatch.setenv("RT_AMD_DEVICES", v)
+        assert_bits_equal(world.render_reference(40, 30), img, f"render() RT_AMD_DEVICES={v}")
+    monkeypatch.setenv("RT_AMD_DEVICES", str(R.device_count() + 1))
+    with pytest.raises(R.RenderError):
+        world.render_reference(40, 30)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _bench_env():
+    env = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        env.pop(k, None)
+    return env
+
+
+def test_bench_single_process_gpus_1():
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "1", "--config",
+                        "c1", "--steps", "3", "--warmup", "1", "--no-cpu-baseline"],
+                       env=_bench_env(), capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = json.loads(r.stdout.strip().splitlines()[-1])
+    assert line["n_gpus"] == 1 and line["rccl_ranks"] == 1 and line["launch"] == "single process"
+    assert line["value"] > 0 and line["rays_per_frame"] > 65536
+
+
+def test_bench_torchrun_two_ranks_rehearsal():
+    """The driver's N>1 launch, two ranks on the one GPU with gloo: HIP tiles,
+    all-gather, and the assembled frame equal to a one-rank render."""
+    env = _bench_env()
+    env.update(RT_BENCH_ONE_DEVICE="1", RT_BENCH_BACKEND="gloo", RT_BENCH_VERIFY="1",
+               OMP_NUM_THREADS="2")
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+                        "--nproc-per-node", "2", "--master-addr", "127.0.0.1", "--master-port",
+                        str(_free_port()), os.path.join(ROOT, "bench.py"), "--gpus", "2",
+                        "--config", "c1", "--steps", "2", "--warmup", "1"],
+                       env=env, capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert "verify: assembled frame == single-rank frame" in r.stderr
+    line = json.loads(r.stdout.strip().splitlines()[-1])
+    assert line["n_gpus"] == 2 and line["rccl_ranks"] == 2

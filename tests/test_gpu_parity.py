@@ -285,7 +285,8 @@ def test_tree_shape_knobs_do_not_change_samples(monkeypatch, scene):
     ref, _ = render_kept(R.World(src), w, h, spp, 8)
     for env in [dict(RT_AMD_LEAF="1"), dict(RT_AMD_LEAF="7"), dict(RT_AMD_TRI_LEAF="2"),
                 dict(RT_AMD_TRI_LEAF="7"), dict(RT_AMD_CAM_LEAF="1"), dict(RT_AMD_CAM_LEAF="5"),
-                dict(RT_AMD_TRI_PHANTOM="0.5"), dict(RT_AMD_BIG_K="2")]:
+                dict(RT_AMD_TRI_PHANTOM="0.5"), dict(RT_AMD_BIG_K="2"),
+                dict(RT_AMD_BIG_K="1e9"), dict(RT_AMD_BIG_K="0")]:
         for k, v in env.items():
             monkeypatch.setenv(k, v)
         out, _ = render_kept(R.World(src), w, h, spp, 8)

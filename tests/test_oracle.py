@@ -258,3 +258,28 @@ def test_ppm_writer_format():  # image.rs:59-81
     lines = txt.split("\n")
     assert lines[:3] == ["P3", "3 2", "255"]
     assert lines[3] == "255 0 0" and lines[8] == "1 2 3" and txt.endswith("\n")
+
+
+def test_emission_matches_numpy_restatement():
+    """Emission (materials.rs:100-102) via the oracle's material hook: the
+    grammar cannot produce it (parser.rs:175-234), so both restatements get
+    the same emitters injected after parsing."""
+    src = scene_text("c_raytracer_world.txt")
+    cam, world = P.parse(src)
+    s = O.Scene(src)
+    for i, rgb in [(4, (4.0, 3.5, 3.0)), (1, (0.0, 0.9, 2.0))]:
+        c, r, _ = world["spheres"][i]
+        world["spheres"][i] = (c, r, ("Emission", tuple(np.float32(x) for x in rgb) + (np.float32(1.0),)))
+        s.set_material(i, 3, rgb)
+    v0, v1, v2, nrm, _ = world["triangles"][1]
+    world["triangles"][1] = (v0, v1, v2, nrm, ("Emission", (np.float32(1.5), np.float32(0.25),
+                                                           np.float32(0.5), np.float32(1.0))))
+    s.set_material(1, 3, (1.5, 0.25, 0.5), triangle=True)
+    w, h, spp, depth = 12, 9, 2, 8
+    ps = np.zeros((w * h * spp, 4), np.float32)
+    a = P.ray_trace(world, cam, w, h, spp, depth, samples=ps)
+    b, _, _, smp = s.render(w, h, spp, depth, record_samples=True)
+    assert np.array_equal(a, b)
+    assert np.array_equal(ps.view(np.uint32), smp.view(np.uint32))
+    base, _, _ = O.Scene(src).render(w, h, spp, depth)
+    assert not np.array_equal(b, base)

@@ -184,6 +184,8 @@ CONFIGS = {
     "c1": (three_spheres, 256, 256, 1, 4),
     "c2": (rtow, 1920, 1080, 64, 8),
     "c3": (rtow, 3840, 2160, 256, 16),
+    # C4 = the C3 frame row-tiled over the GPUs (bench.py --gpus 8 --config c4)
+    "c4": (rtow, 3840, 2160, 256, 16),
     "c5": (mesh, 1920, 1080, 64, 8),
 }
 
