@@ -86,6 +86,14 @@ def lib(path=None):
     """The loaded library (another build can be loaded side by side for A/B runs)."""
     path = path or LIB_PATH
     if path not in _libs:
+        # One HIP runtime per process: torch ships its own libamdhip64.so.7 /
+        # librccl.so.1 (same sonames as /opt/rocm's).  Whichever loads first
+        # serves both, and torch cannot initialise on /opt/rocm's runtime
+        # ("No HIP GPUs are available"), so torch is loaded first when present.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         if not os.path.exists(path):
             raise RenderError(f"{path} is missing: run `make -C {HERE}` (build())")
         L = C.CDLL(path)

@@ -78,7 +78,9 @@ def test_c4_eight_tiles_reassemble_to_c3(rtow, c3_frame):
     rays = 0
     for rank in range(nranks):
         tile, st = world.render(W, H, spp, depth, row_block=block, rank=rank, nranks=nranks)
-        assert tile.shape == (R.tile_rows(H, block, rank, nranks), W, 4) == (270, W, 4)
+        # 270 blocks of 8 rows over 8 ranks: 34 blocks (272 rows) or 33 (264)
+        assert tile.shape == (R.tile_rows(H, block, rank, nranks), W, 4)
+        assert tile.shape[0] in (264, 272)
         rays += st["rays"]
         rows = [R.tile_row(k, block, rank, nranks) for k in range(tile.shape[0])]
         asm[rows] = tile
