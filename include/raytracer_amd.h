@@ -17,12 +17,17 @@ extern "C" {
 /* RNG modes.  The reference draws every sample from ONE xorshift32 stream
  * seeded 2547549 for the whole frame (common.rs:321, random.rs:8-10), which
  * is a sequential dependency.  The GPU offers:
+ *   RT_RNG_SERIAL: that stream, seeded `seed`: the reference's own frame, bit
+ *     for bit.  The library finds every sample's start state on the GPU
+ *     (chunked candidate tables and walks), then renders as
+ *     REPLAY; width*height*spp must be below 2^32.  The default of render().
  *   RT_RNG_COUNTER: sample (pixel p, index s) starts xorshift32 from
  *     rt_sample_seed(seed, p*spp + s); draws inside a sample follow the
- *     reference order exactly.  Default.
+ *     reference order exactly.  The fast mode (no sequential dependency);
+ *     statistically, not bitwise, equal to the reference.
  *   RT_RNG_REPLAY: sample start states are read from a table (e.g. recorded
  *     from a serial CPU run), which reproduces the serial frame bit-for-bit. */
-enum { RT_RNG_COUNTER = 1, RT_RNG_REPLAY = 2 };
+enum { RT_RNG_COUNTER = 1, RT_RNG_REPLAY = 2, RT_RNG_SERIAL = 3 };
 
 typedef struct RtRenderOptions {
   int32_t samples_per_pixel;      /* Options.samples_per_pixel (common.rs:290) */
@@ -85,6 +90,8 @@ typedef struct RtRenderStats {
   uint32_t tri_bvh;          /* 1 when the triangle BVH ran                   */
   uint32_t fused_resolve;    /* 1 when the trace kernel resolved the pixels
                                 (no slab, resolve_ms ~ 0)                    */
+  double serial_ms;          /* RT_RNG_SERIAL: HIP-event time spent finding the
+                                start states (before the REPLAY render)       */
 } RtRenderStats;
 
 /* spp 16, depth 8 (lib.rs:51), COUNTER, seed 2547549, one rank, device -1,

@@ -10,6 +10,12 @@
 namespace rtamd {
 
 enum : uint32_t { kRngCounter = 1, kRngReplay = 2 };
+// SERIAL-mode passes (runtime.cpp render_frame_serial), kernel-internal modes:
+// jobs are (sample, variant) pairs and store the sample's diffuse/metal scatter
+// count b (the reference draws 2 + 3b numbers per sample) instead of a colour.
+//   kRngSerialCount: variant k = candidate; start state win[2 jl + 3 (lo[jl] + k)]
+//   kRngSerialEstimate: variant r = repetition; start state counter_seed(seed, j * V + r)
+enum : uint32_t { kRngSerialCount = 3, kRngSerialEstimate = 4 };
 enum : uint32_t { kMatDiffuse = 0, kMatMetal = 1, kMatDielectric = 2, kMatEmission = 3 };
 constexpr uint32_t kPrimaryTriStripW = 8;  // bvh.h kTriStripW
 constexpr uint32_t kTraceRing = 4;         // chunk slots per wave (fused resolve)
@@ -94,9 +100,30 @@ struct TraceParams {
     // primary-ray sphere candidates (bvh.h PrimarySphereLists, sphere-only
     // scenes): per image pixel (i0 | i1 << 16, i2 | count << 16); nullptr: walk
     const uint2 *spl;
+    // SERIAL-mode passes (mode kRngSerialCount / kRngSerialEstimate): p.spp is
+    // the variants per sample V and p.npix the samples of the launch; launch
+    // sample jl is sample cbase + jl of the frame (reference order, common.rs:327-336)
+    const uint32_t *win;      // kRngSerialCount: stream states from the chunk's first sample's start
+    const uint32_t *lo;       // kRngSerialCount: per chunk sample, its first candidate (B offset)
+    const uint32_t *ctrl;     // serial control block: ctrl[0] != 0 (a walk failed) -> exit at once
+    uint32_t cbase;           // first frame sample of the launch
+    uint32_t sspp;            // the frame's spp ...
+    FastDiv div_sspp;         // ... and its divider
+    uint32_t max_draws;       // 2 + 3 * max(depth, 0): bound of the draw count search
 };
 
 hipError_t launch_trace(const TraceParams &p, uint32_t blocks, hipStream_t stream);
+// SERIAL mode.  ctrl: u32 {fail, state at the chunk's first sample, sum of b, failing chunk}.
+// jump: 64 x 32 u32, column c of M^(2^i) (xorshift32 is linear over GF(2)).
+// Window: win[i] = xorshift32^i(ctrl[1]) for i < n.
+hipError_t launch_serial_window(const uint32_t *ctrl, const uint32_t *jump, uint32_t *win, uint32_t n,
+                                hipStream_t stream);
+// Walk: the chunk's true path through the candidate table (b of sample jl at
+// candidate k = table[jl * K + k], plane 0 of a slab), writing each sample's
+// start state to states[jl] and the next chunk's start state to ctrl[1].
+hipError_t launch_serial_walk(uint32_t *ctrl, const float *table, const uint32_t *lo,
+                              const uint32_t *win, uint32_t *states, uint32_t nsamples, uint32_t K,
+                              uint32_t chunk, hipStream_t stream);
 // inv_spp = 1.0 / (spp as f32) computed from the signed spp (common.rs:345).
 hipError_t launch_resolve_ex(const float *samples, uint32_t *out, uint32_t npix, uint32_t spp,
                              float inv_spp, uint32_t width, uint32_t slab_row0,

@@ -525,6 +525,16 @@ __device__ __forceinline__ void tri_leaf(const TraceParams &p, F3 org, F3 dir, b
 // row counts from the bottom as ray_trace does (common.rs:327-331).
 __device__ __forceinline__ void job_pixel(const TraceParams &p, uint32_t job, uint32_t &s,
                                           uint32_t &col, uint32_t &row) {
+    if (p.mode >= kRngSerialCount) {
+        // SERIAL passes: job = launch sample * V + variant; frame sample j =
+        // (row * W + col) * spp + s in the reference's loop order (common.rs:327-336)
+        const uint32_t j = p.cbase + fdiv(job, p.div_spp);
+        const uint32_t pix = fdiv(j, p.div_sspp);
+        s = j - pix * p.sspp;
+        row = fdiv(pix, p.div_width);
+        col = pix - row * p.width;
+        return;
+    }
     const uint32_t lp = fdiv(job, p.div_spp);
     s = job - lp * p.spp;
     const uint32_t q = fdiv(lp, p.div_width);
@@ -533,6 +543,14 @@ __device__ __forceinline__ void job_pixel(const TraceParams &p, uint32_t job, ui
     const uint32_t blk = fdiv(lr, p.div_rowblock);
     const uint32_t ir = (blk * p.nranks + p.rank) * p.row_block + (lr - blk * p.row_block);
     row = p.height - 1u - ir;
+}
+
+// SERIAL passes: the start state of job (launch sample jl, variant k).
+__device__ __forceinline__ uint32_t serial_start(const TraceParams &p, uint32_t job) {
+    const uint32_t jl = fdiv(job, p.div_spp);
+    const uint32_t k = job - jl * p.spp;
+    if (p.mode == kRngSerialCount) return p.win[2u * jl + 3u * (p.lo[jl] + k)];
+    return counter_seed(p.seed, (uint64_t)(p.cbase + jl) * p.spp + k);
 }
 
 // Primary ray against its pixel strip's candidate records (bvh.h
@@ -667,6 +685,8 @@ template <bool kBvh, bool kLds, bool kStep, bool kMesh, bool kCount>
 __global__ __launch_bounds__(kLds ? (kMesh ? RT_LDS_BLOCK_MESH : RT_LDS_BLOCK_SPHERES) : 256)
 __attribute__((amdgpu_waves_per_eu((kMesh && !kCount) ? RT_WAVES_PER_EU_MESH : RT_WAVES_PER_EU, 8)))
 void trace_kernel(TraceParams p) {
+    // SERIAL passes: a failed walk cancels the rest of the frame's launches
+    if (p.ctrl != nullptr && p.ctrl[0] != 0u) return;
     const uint32_t lane = __lane_id();
     extern __shared__ float4 lds[];
     BvhView view;
@@ -980,6 +1000,20 @@ void trace_kernel(TraceParams p) {
             }
             RT_STAMP(3);
             if (done) {
+                if (p.mode >= kRngSerialCount) {
+                    // SERIAL passes: the sample's scatter count b instead of its
+                    // colour -- the draws it consumed (2 + 3b, common.rs:335-336 and
+                    // random_unit_sphere per diffuse/metal scatter, common.rs:32-38)
+                    // are the steps from its start state to its end state
+                    uint32_t x = serial_start(p, slot), n = 0;
+                    while (x != rng && n < p.max_draws) {
+                        x ^= x << 13;
+                        x ^= x >> 17;
+                        x ^= x << 5;
+                        ++n;
+                    }
+                    out_r = (x == rng && n >= 2u) ? (float)((n - 2u) / 3u) : -1.0f;
+                }
                 // planar (R, G, B planes): 12 B per sample, to the slab or the ring
                 sbase[slot] = out_r;
                 sbase[pstride + slot] = out_g;
@@ -1066,8 +1100,12 @@ void trace_kernel(TraceParams p) {
                 uint32_t s, col, row;
                 job_pixel(p, job, s, col, row);
                 slot = job + cur_off;
-                const uint64_t gjob = ((uint64_t)row * p.width + col) * p.spp + s;
-                rng = (p.mode == kRngReplay) ? p.replay[gjob] : counter_seed(p.seed, gjob);
+                if (p.mode >= kRngSerialCount) {
+                    rng = serial_start(p, job);
+                } else {
+                    const uint64_t gjob = ((uint64_t)row * p.width + col) * p.spp + s;
+                    rng = (p.mode == kRngReplay) ? p.replay[gjob] : counter_seed(p.seed, gjob);
+                }
                 // common.rs:335-337: u drawn before v; camera.rs:84-89
                 // numerators are in [2^-32, 2^24]: exactdiv.h with the host's
                 // reciprocals whenever the denominators are in range
@@ -1283,6 +1321,73 @@ hipError_t trace_occupancy(int *blocks_per_cu, int variant, size_t lds_bytes, bo
                            bool count) {
     return count ? trace_occupancy_c<true>(blocks_per_cu, variant, lds_bytes, step, tri)
                  : trace_occupancy_c<false>(blocks_per_cu, variant, lds_bytes, step, tri);
+}
+
+// ------------------------------------------------------------ SERIAL mode
+// The reference draws every sample from ONE xorshift32 stream (common.rs:321):
+// sample j starts at stream position P_j = 2j + 3B_j, B_j = the diffuse/metal
+// scatters of all earlier samples.  runtime.cpp render_frame_serial finds
+// every P_j chunk by chunk: trace_kernel (kRngSerialCount) traces each sample
+// of the chunk from K candidate positions around its predicted one,
+// serial_walk_kernel follows the true path through that table, and the frame
+// is then rendered in REPLAY mode from the start states found.
+
+// xorshift32^(2^i) as 32 columns (GF(2) matrix): y = XOR of columns c with bit c of x set
+__device__ __forceinline__ uint32_t gf2_apply(const uint32_t *cols, uint32_t x) {
+    uint32_t y = 0;
+#pragma unroll 8
+    for (uint32_t c = 0; c < 32u; ++c) y ^= (x >> c & 1u) ? cols[c] : 0u;
+    return y;
+}
+
+__global__ __launch_bounds__(256) void serial_window_kernel(const uint32_t *__restrict__ ctrl,
+                                                            const uint32_t *__restrict__ jump,
+                                                            uint32_t *__restrict__ win, uint32_t n) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (ctrl[0] != 0u || i >= n) return;
+    uint32_t x = ctrl[1];
+    for (uint32_t b = 0; (i >> b) != 0u; ++b)
+        if ((i >> b) & 1u) x = gf2_apply(jump + 32u * b, x);
+    win[i] = x;
+}
+
+__global__ __launch_bounds__(64) void serial_walk_kernel(uint32_t *__restrict__ ctrl,
+                                                         const float *__restrict__ table,
+                                                         const uint32_t *__restrict__ lo,
+                                                         const uint32_t *__restrict__ win,
+                                                         uint32_t *__restrict__ states, uint32_t nsamples,
+                                                         uint32_t K, uint32_t chunk) {
+    if (threadIdx.x != 0 || ctrl[0] != 0u) return;
+    uint32_t B = 0;  // scatters since the chunk's first sample
+    for (uint32_t jl = 0; jl < nsamples; ++jl) {
+        const uint32_t l = lo[jl];
+        const float b = (B >= l && B - l < K) ? table[(size_t)jl * K + (B - l)] : -1.0f;
+        if (!(b >= 0.0f)) {  // outside the candidate window (or no count): retry wider
+            ctrl[3] = chunk;
+            ctrl[0] = 1u;
+            return;
+        }
+        states[jl] = win[2u * jl + 3u * B];
+        B += (uint32_t)b;
+    }
+    ctrl[1] = win[2u * nsamples + 3u * B];
+    ctrl[2] += B;
+}
+
+hipError_t launch_serial_window(const uint32_t *ctrl, const uint32_t *jump, uint32_t *win, uint32_t n,
+                                hipStream_t stream) {
+    if (!n) return hipSuccess;
+    hipLaunchKernelGGL(serial_window_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, ctrl, jump,
+                       win, n);
+    return hipGetLastError();
+}
+
+hipError_t launch_serial_walk(uint32_t *ctrl, const float *table, const uint32_t *lo,
+                              const uint32_t *win, uint32_t *states, uint32_t nsamples, uint32_t K,
+                              uint32_t chunk, hipStream_t stream) {
+    hipLaunchKernelGGL(serial_walk_kernel, dim3(1), dim3(64), 0, stream, ctrl, table, lo, win, states,
+                       nsamples, K, chunk);
+    return hipGetLastError();
 }
 
 // Multi-device frames (runtime.cpp render_frame_multi): rank g's tile holds

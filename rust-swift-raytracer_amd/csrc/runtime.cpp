@@ -51,10 +51,13 @@ DeviceState::~DeviceState() {
     void *bufs[] = {sph_hot, sph_cold, tri_hot, tri_geo, mats, samples, ring, out, replay, counter, stats,
                     bvh_nodes, bvh_prims, big_hot, bvh_miss, bvh_prim_id, big_id, bvh_miss16,
                     sph_shade, sph_kind, tbvh_nodes, tbvh_tris, tbvh_loose,
-                    cam_nodes, cam_tris, ptl_off, ptl_items, spl, tile, gath};
+                    cam_nodes, cam_tris, ptl_off, ptl_items, spl, tile, gath,
+                    sstates, slo, swin, sjump, sctrl};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
     for (hipEvent_t e : ev)
+        if (e) (void)hipEventDestroy(e);
+    for (hipEvent_t e : sev)
         if (e) (void)hipEventDestroy(e);
     if (done) (void)hipEventDestroy(done);
     if (stream) (void)hipStreamDestroy(stream);
@@ -97,6 +100,7 @@ static int device_for(WorldState &w, int want, DeviceState *&out) {
         d->device = dev;
         HIP_TRY(hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking));
         for (auto &e : d->ev) HIP_TRY(hipEventCreate(&e));
+        for (auto &e : d->sev) HIP_TRY(hipEventCreate(&e));
         HIP_TRY(hipEventCreateWithFlags(&d->done, hipEventDisableTiming));
         hipDeviceProp_t prop;
         HIP_TRY(hipGetDeviceProperties(&prop, dev));
@@ -245,15 +249,21 @@ static hipError_t grow(T *&buf, size_t &cap, size_t n) {
 
 int render_frame(WorldState &w, const CameraModel &cam, size_t width, size_t height,
                  const RtRenderOptions &o, uint32_t *d_out, hipStream_t stream,
-                 RtRenderStats *stats) {
+                 RtRenderStats *stats, const SerialPass *sp, const uint32_t *d_replay) {
     if (stats) std::memset(stats, 0, sizeof(*stats));
     const uint32_t nranks = o.nranks ? o.nranks : 1;
     if (o.rank >= nranks) { set_error("rank >= nranks"); return -1; }
-    if (o.rng_mode != RT_RNG_COUNTER && o.rng_mode != RT_RNG_REPLAY) {
-        set_error("rng_mode must be RT_RNG_COUNTER or RT_RNG_REPLAY");
+    if (o.rng_mode == RT_RNG_SERIAL && !sp && !d_replay)
+        return render_frame_serial(w, cam, width, height, o, d_out, stream, stats);
+    if (!sp && o.rng_mode != RT_RNG_COUNTER && o.rng_mode != RT_RNG_REPLAY && !d_replay) {
+        set_error("rng_mode must be RT_RNG_COUNTER, RT_RNG_REPLAY or RT_RNG_SERIAL");
         return -1;
     }
-    if (o.rng_mode == RT_RNG_REPLAY && !o.replay_states) { set_error("replay table missing"); return -1; }
+    if (o.rng_mode == RT_RNG_REPLAY && !o.replay_states && !d_replay) {
+        set_error("replay table missing");
+        return -1;
+    }
+    if (sp) d_out = reinterpret_cast<uint32_t *>(1);  // (a pass writes counts, not pixels)
     if (width > 0xFFFFFFu || height > 0xFFFFFFu) { set_error("frame too large"); return -1; }
     const uint32_t B = nranks > 1 ? (o.row_block ? o.row_block : 1) : (uint32_t)std::max<size_t>(height, 1);
     const size_t T = tile_rows(height, B, o.rank, nranks);
@@ -285,7 +295,8 @@ int render_frame(WorldState &w, const CameraModel &cam, size_t width, size_t hei
     if (jobs_per_row && !fused)
         HIP_TRY(grow(d->samples, d->samples_cap, 3 * rows_per_slab * jobs_per_row));
 
-    if (o.rng_mode == RT_RNG_REPLAY && spp) {
+    const bool replay = d_replay != nullptr || o.rng_mode == RT_RNG_REPLAY;
+    if (!d_replay && !sp && o.rng_mode == RT_RNG_REPLAY && spp) {
         const size_t n = width * height * (size_t)spp;
         HIP_TRY(grow(d->replay, d->replay_cap, n));
         HIP_TRY(hipMemcpyAsync(d->replay, o.replay_states, n * 4, hipMemcpyHostToDevice, s));
@@ -297,7 +308,7 @@ int render_frame(WorldState &w, const CameraModel &cam, size_t width, size_t hei
     p.mats = d->mats;
     p.samples = d->samples;
     p.job_counter = d->counter;
-    p.replay = d->replay;
+    p.replay = d_replay ? d_replay : d->replay;
     const Vec3 cv[4] = {cam.origin, cam.lower_left, cam.horizontal, cam.vertical};
     for (int i = 0; i < 4; ++i) { p.cam[3 * i] = cv[i].x; p.cam[3 * i + 1] = cv[i].y; p.cam[3 * i + 2] = cv[i].z; }
     p.wden = (float)(uint64_t)(width - 1);   // (width-1) as f32 (common.rs:335)
@@ -311,7 +322,8 @@ int render_frame(WorldState &w, const CameraModel &cam, size_t width, size_t hei
     p.nsph = d->nsph; p.nsph_padded = d->nsph_padded; p.ntri = d->ntri;
     p.width = (uint32_t)width; p.height = (uint32_t)height; p.spp = spp;
     p.depth = o.max_ray_bounces;
-    p.mode = o.rng_mode; p.seed = o.seed;
+    p.mode = replay ? (uint32_t)RT_RNG_REPLAY : (uint32_t)RT_RNG_COUNTER;
+    p.seed = o.seed;
     p.ablate = (uint32_t)env_u64("RT_AMD_ABLATE", 0);
     p.sph_shade = d->sph_shade;
     p.sph_kind = d->sph_kind;
@@ -453,6 +465,46 @@ int render_frame(WorldState &w, const CameraModel &cam, size_t width, size_t hei
         HIP_TRY(hipMemsetAsync(d->stats, 0, max_waves * kStatSlots * 8, s));
         p.stats = d->stats;
     }
+    if (sp) {
+        // one SERIAL pass: nsamples x variants jobs (job = launch sample *
+        // variants + variant); each stores its scatter count to slab plane 0
+        const uint64_t njobs = (uint64_t)sp->nsamples * sp->variants;
+        if (njobs == 0) return 0;
+        if (njobs > 0x7FFFFFFFull) { set_error("serial pass too large"); return -1; }
+        HIP_TRY(grow(d->samples, d->samples_cap, 3 * njobs));
+        p.samples = d->samples;
+        p.ring = nullptr;
+        p.ring_shift = 0;
+        p.mode = sp->mode;
+        p.spp = sp->variants;
+        p.div_spp = make_fastdiv(sp->variants);
+        p.sspp = spp;
+        p.div_sspp = make_fastdiv(spp ? spp : 1);
+        p.cbase = sp->cbase;
+        p.win = sp->win;
+        p.lo = sp->lo;
+        p.ctrl = sp->ctrl;
+        p.max_draws = 2u + 3u * (uint32_t)std::max(o.max_ray_bounces, 0);
+        p.njobs = (uint32_t)njobs;
+        p.npix = sp->nsamples;
+        p.slab_row0 = 0;
+        const uint64_t jobs_per_block = waves_per_block * 256;
+        const uint64_t blocks = std::max<uint64_t>(
+            1, std::min<uint64_t>(full_blocks, (njobs + jobs_per_block - 1) / jobs_per_block));
+        const uint64_t nwaves = blocks * waves_per_block;
+        uint64_t chunk = std::min<uint64_t>(256, std::max<uint64_t>(64, njobs / (nwaves * 16) / 64 * 64));
+        chunk = chunk >= sp->variants ? chunk / sp->variants * sp->variants : sp->variants;
+        p.chunk = (uint32_t)chunk;
+        const uint64_t parts = std::max<uint64_t>(
+            1, std::min<uint64_t>({(uint64_t)(p.step ? 64 : 16), kMaxParts, njobs / (16 * chunk) + 1}));
+        p.nparts = (uint32_t)parts;
+        HIP_TRY(hipMemsetAsync(d->counter, 0, parts * 128, s));
+        HIP_TRY(launch_trace(p, (uint32_t)blocks, s));
+        HIP_TRY(hipEventRecord(d->done, s));
+        d->done_stream = s;
+        d->last_jobs = 0;  // the slab holds counts now, not samples
+        return 0;
+    }
     for (size_t r0 = 0; r0 < T; r0 += rows_per_slab) {
         const size_t rows = std::min(rows_per_slab, T - r0);
         const uint64_t njobs = rows * jobs_per_row;
@@ -551,6 +603,202 @@ int render_frame(WorldState &w, const CameraModel &cam, size_t width, size_t hei
         stats->tri_bvh = use_tbvh ? 1u : 0u;
         stats->fused_resolve = fused ? 1u : 0u;
         stats->bvh_tri_tests = use_tbvh ? st[9] : stats->tri_tests;
+    }
+    return 0;
+}
+
+// ------------------------------------------------------------ SERIAL mode
+// The reference draws every sample from one xorshift32 stream seeded 2547549
+// (common.rs:321, random.rs:8-30): sample j (reference order (row * W + col)
+// * spp + s) starts at stream position P_j = 2j + 3 B_j, where B_j counts the
+// diffuse/metal scatters of all earlier samples (2 draws for u, v, 3 per
+// random_unit_sphere).  That is a sequential dependency, resolved here on the
+// device chunk by chunk:
+//   1. estimate: each sample traced R times from counter seeds gives every
+//      pixel's mean scatter count (kRngSerialEstimate);
+//   2. per chunk of L samples, whose first sample's B is known exactly:
+//      window: the stream states from that sample's start on (jump matrices);
+//      count: every sample traced from K candidate positions centred on its
+//        predicted offset (kRngSerialCount), a table of scatter counts;
+//      walk: one lane follows the true path through the table, writing each
+//        sample's start state and the next chunk's start state;
+//      a walk that leaves its window cancels the remaining launches and the
+//      host resumes from that chunk with a window twice as wide;
+//   3. the frame is rendered in REPLAY mode from the start states.
+// The result is the reference's own frame, bit for bit (tests/test_gpu_serial.py).
+namespace {
+uint32_t xorshift32(uint32_t x) {
+    x ^= x << 13;
+    x ^= x >> 17;
+    x ^= x << 5;
+    return x;
+}
+
+// columns of M^(2^i), i < 64, M the xorshift32 step as a GF(2) matrix
+std::vector<uint32_t> xorshift_jump_table() {
+    std::vector<uint32_t> t(64 * 32);
+    for (uint32_t c = 0; c < 32; ++c) t[c] = xorshift32(1u << c);
+    auto apply = [&](const uint32_t *cols, uint32_t x) {
+        uint32_t y = 0;
+        for (uint32_t c = 0; c < 32; ++c)
+            if (x >> c & 1u) y ^= cols[c];
+        return y;
+    };
+    for (int i = 1; i < 64; ++i)
+        for (uint32_t c = 0; c < 32; ++c) t[32 * i + c] = apply(&t[32 * (i - 1)], t[32 * (i - 1) + c]);
+    return t;
+}
+}  // namespace
+
+int render_frame_serial(WorldState &w, const CameraModel &cam, size_t width, size_t height,
+                        const RtRenderOptions &o, uint32_t *d_out, hipStream_t stream,
+                        RtRenderStats *stats) {
+    if (stats) std::memset(stats, 0, sizeof(*stats));
+    if (width == 0 || height == 0) return 0;
+    const uint64_t spp = (uint64_t)std::max(o.samples_per_pixel, 0);
+    const uint64_t N = (uint64_t)width * height * spp;
+    if (N >= 0xFFFFFFFFull) {
+        set_error("RT_RNG_SERIAL: width * height * spp must be below 2^32");
+        return -1;
+    }
+    if (o.max_ray_bounces > 100000) {
+        set_error("RT_RNG_SERIAL: max_ray_bounces above 100000");
+        return -1;
+    }
+    const uint32_t depth = (uint32_t)std::max(o.max_ray_bounces, 0);
+    std::lock_guard<std::recursive_mutex> lock(w.mu);
+    DeviceState *d = nullptr;
+    int rc = device_for(w, o.device, d);
+    if (rc) return rc;
+    hipStream_t s = stream ? stream : d->stream;
+    if (d->done_stream && d->done_stream != s) HIP_TRY(hipStreamWaitEvent(s, d->done, 0));
+    HIP_TRY(hipEventRecord(d->sev[0], s));
+    HIP_TRY(grow(d->sstates, d->sstates_cap, std::max<uint64_t>(N, 1)));
+    RtRenderOptions ob = o;
+    ob.rng_mode = RT_RNG_COUNTER;
+    ob.rank = 0;
+    ob.nranks = 1;
+    ob.flags = 0;
+    if (N > 0) {
+        // 1. per-pixel mean scatter counts from R counter-seeded traces per sample
+        const uint64_t R = std::max<uint64_t>(
+            1, std::min<uint64_t>({(64 + spp - 1) / spp, 16, 0x7FFFFFFFull / N}));
+        const uint64_t npix = (uint64_t)width * height;
+        std::vector<double> mu(npix, 0.0);
+        double ss = 0.0;  // within-pixel sum of squares (sigma of one sample's b)
+        {
+            std::vector<float> est;
+            std::vector<double> sq(npix, 0.0);
+            const uint64_t step = std::max<uint64_t>(1, (1ull << 28) / R);
+            for (uint64_t c0 = 0; c0 < N; c0 += step) {
+                const uint32_t n = (uint32_t)std::min<uint64_t>(step, N - c0);
+                const SerialPass sp{kRngSerialEstimate, (uint32_t)c0, n, (uint32_t)R, nullptr, nullptr,
+                                    nullptr};
+                rc = render_frame(w, cam, width, height, ob, nullptr, s, nullptr, &sp);
+                if (rc) return rc;
+                est.resize((size_t)n * R);
+                HIP_TRY(hipMemcpyAsync(est.data(), d->samples, est.size() * 4, hipMemcpyDeviceToHost, s));
+                HIP_TRY(hipStreamSynchronize(s));
+                for (uint64_t i = 0; i < est.size(); ++i) {
+                    const float b = est[i];
+                    if (!(b >= 0.0f)) {
+                        set_error("RT_RNG_SERIAL: estimate pass lost a sample's draw count");
+                        return -5;
+                    }
+                    const uint64_t pix = (c0 + i / R) / spp;
+                    mu[pix] += b;
+                    sq[pix] += (double)b * b;
+                }
+            }
+            const double per = (double)(spp * R);
+            for (uint64_t q = 0; q < npix; ++q) {
+                mu[q] /= per;
+                ss += sq[q] - per * mu[q] * mu[q];
+            }
+        }
+        const double sigma = std::sqrt(std::max(ss, 0.0) / (double)(N * R)) + 0.05;
+        // 2. chunks of L samples, K candidates per sample
+        const uint64_t L = std::max<uint64_t>(1, std::min<uint64_t>(env_u64("RT_AMD_SERIAL_CHUNK", 2048), N));
+        const double spread = std::sqrt((double)L * (1.0 + 1.0 / (double)(spp * R)));
+        uint64_t K = (uint64_t)std::ceil(2.0 * 6.0 * sigma * spread) + 16;
+        if (const uint64_t k = env_u64("RT_AMD_SERIAL_K", 0)) K = k;  // (tests: force retries)
+        K = std::min<uint64_t>(std::max<uint64_t>(K, 4), (uint64_t)depth * L + 1);
+        const uint64_t nchunks = (N + L - 1) / L;
+        std::vector<uint32_t> lo(N);
+        std::vector<uint64_t> wlen(nchunks);
+        auto place = [&](uint64_t Kc) {  // candidate offsets and window lengths for K = Kc
+            for (uint64_t c = 0; c < nchunks; ++c) {
+                const uint64_t a = c * L, n = std::min<uint64_t>(L, N - a);
+                double acc = 0.0;
+                uint64_t need = 0;
+                for (uint64_t jl = 0; jl < n; ++jl) {
+                    const double centre = std::floor(acc) - (double)(Kc / 2);
+                    const double hi = (double)depth * (double)jl;
+                    const uint64_t l = (uint64_t)std::min(std::max(centre, 0.0), hi);
+                    lo[a + jl] = (uint32_t)l;
+                    need = std::max<uint64_t>(need, 2 * jl + 3 * (l + Kc));
+                    acc += mu[(a + jl) / spp];
+                }
+                wlen[c] = need + 3 * (uint64_t)depth + 3;
+            }
+        };
+        if (!d->sjump) {
+            const std::vector<uint32_t> jt = xorshift_jump_table();
+            HIP_TRY(hipMalloc((void **)&d->sjump, jt.size() * 4));
+            HIP_TRY(hipMemcpy(d->sjump, jt.data(), jt.size() * 4, hipMemcpyHostToDevice));
+        }
+        if (!d->sctrl) HIP_TRY(hipMalloc((void **)&d->sctrl, 16));
+        HIP_TRY(grow(d->slo, d->slo_cap, N));
+        const uint32_t ctrl0[4] = {0u, o.seed, 0u, 0u};  // Random::new() state (random.rs:8-10)
+        HIP_TRY(hipMemcpyAsync(d->sctrl, ctrl0, 16, hipMemcpyHostToDevice, s));
+        uint64_t c_from = 0;
+        for (int attempt = 0;; ++attempt) {
+            place(K);
+            const uint64_t wmax = *std::max_element(wlen.begin(), wlen.end());
+            if (wmax >= 0xFFFFFFFFull || (uint64_t)L * K > 0x7FFFFFFFull) {
+                set_error("RT_RNG_SERIAL: candidate window too large");
+                return -5;
+            }
+            HIP_TRY(grow(d->swin, d->swin_cap, wmax));
+            HIP_TRY(hipMemcpyAsync(d->slo, lo.data(), N * 4, hipMemcpyHostToDevice, s));
+            for (uint64_t c = c_from; c < nchunks; ++c) {
+                const uint64_t a = c * L, n = std::min<uint64_t>(L, N - a);
+                HIP_TRY(launch_serial_window(d->sctrl, d->sjump, d->swin, (uint32_t)wlen[c], s));
+                const SerialPass sp{kRngSerialCount, (uint32_t)a, (uint32_t)n, (uint32_t)K, d->swin,
+                                    d->slo + a, d->sctrl};
+                rc = render_frame(w, cam, width, height, ob, nullptr, s, nullptr, &sp);
+                if (rc) return rc;
+                HIP_TRY(launch_serial_walk(d->sctrl, d->samples, d->slo + a, d->swin, d->sstates + a,
+                                           (uint32_t)n, (uint32_t)K, (uint32_t)c, s));
+            }
+            uint32_t ctrl[4];
+            HIP_TRY(hipMemcpyAsync(ctrl, d->sctrl, 16, hipMemcpyDeviceToHost, s));
+            HIP_TRY(hipStreamSynchronize(s));
+            if (ctrl[0] == 0) break;
+            // a walk left its window: resume from that chunk (its start state is
+            // still in ctrl[1]) with twice the candidates
+            if (attempt >= 6 || K >= (uint64_t)depth * L + 1) {
+                set_error("RT_RNG_SERIAL: walk left the candidate window");
+                return -5;
+            }
+            c_from = ctrl[3];
+            K = std::min<uint64_t>(2 * K, (uint64_t)depth * L + 1);
+            const uint32_t zero = 0;
+            HIP_TRY(hipMemcpyAsync(d->sctrl, &zero, 4, hipMemcpyHostToDevice, s));
+        }
+    }
+    HIP_TRY(hipEventRecord(d->sev[1], s));
+    // 3. the frame (or rank's tile) from the start states
+    RtRenderOptions orp = o;
+    orp.rng_mode = RT_RNG_REPLAY;
+    orp.replay_states = nullptr;
+    rc = render_frame(w, cam, width, height, orp, d_out, s, stats, nullptr, d->sstates);
+    if (rc) return rc;
+    if (stats) {
+        float ms = 0.0f;
+        HIP_TRY(hipEventSynchronize(d->sev[1]));
+        HIP_TRY(hipEventElapsedTime(&ms, d->sev[0], d->sev[1]));
+        stats->serial_ms = ms;
     }
     return 0;
 }

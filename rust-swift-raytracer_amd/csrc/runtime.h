@@ -27,6 +27,7 @@ struct DeviceState {
     int device = -1;
     hipStream_t stream = nullptr;
     hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
+    hipEvent_t sev[2] = {nullptr, nullptr};  // SERIAL mode: start-state search
     float4 *sph_hot = nullptr, *sph_cold = nullptr, *tri_hot = nullptr, *tri_geo = nullptr;
     float *mats = nullptr;
     float4 *sph_shade = nullptr;
@@ -57,6 +58,13 @@ struct DeviceState {
     hipEvent_t done = nullptr;       // end of the last frame enqueued on this device ...
     hipStream_t done_stream = nullptr;  // ... and the stream it was enqueued on
     uint32_t *replay = nullptr;      size_t replay_cap = 0;
+    // SERIAL mode (render_frame_serial): start states, candidate offsets, the
+    // stream window of a chunk, xorshift jump matrices, control block
+    uint32_t *sstates = nullptr;     size_t sstates_cap = 0;
+    uint32_t *slo = nullptr;         size_t slo_cap = 0;
+    uint32_t *swin = nullptr;        size_t swin_cap = 0;
+    uint32_t *sjump = nullptr;
+    uint32_t *sctrl = nullptr;
     uint32_t *counter = nullptr;                                // job counter
     unsigned long long *stats = nullptr; size_t stats_cap = 0;  // per-wave counter records
     // resident workgroups per CU of each kernel variant, [0]: whole walks, [1]: sliced walks
@@ -90,11 +98,31 @@ struct WorldState {
     std::recursive_mutex mu;
 };
 
+// One launch of a SERIAL-mode pass (render_frame_serial): the frame's jobs are
+// replaced by nsamples x variants jobs starting at frame sample cbase, each
+// storing its sample's diffuse/metal scatter count to plane 0 of the slab
+// (DeviceState::samples) instead of a colour (render.h kRngSerial*).
+struct SerialPass {
+    uint32_t mode;            // kRngSerialCount or kRngSerialEstimate
+    uint32_t cbase, nsamples, variants;
+    const uint32_t *win, *lo, *ctrl;
+};
+
 // Renders rank's tile of a width x height frame into device memory d_out
 // (RGBA8 words, tile row-major).  stream may be null (library stream).
+// sp: launch that SERIAL pass instead (d_out unused).  d_replay: REPLAY from
+// this device-resident start-state table (frame sample order).
 int render_frame(WorldState &w, const CameraModel &cam, size_t width, size_t height,
                  const RtRenderOptions &opts, uint32_t *d_out, hipStream_t stream,
-                 RtRenderStats *stats);
+                 RtRenderStats *stats, const SerialPass *sp = nullptr,
+                 const uint32_t *d_replay = nullptr);
+
+// RT_RNG_SERIAL: the reference's single frame-wide xorshift32 stream
+// (common.rs:321).  Finds every sample's start state on the device (chunked
+// candidate tables + walks), then renders in REPLAY mode.
+int render_frame_serial(WorldState &w, const CameraModel &cam, size_t width, size_t height,
+                        const RtRenderOptions &opts, uint32_t *d_out, hipStream_t stream,
+                        RtRenderStats *stats);
 
 // A frame row-tiled over opts.ndevices devices (first = opts.device, or the
 // current device) in this one process: each device renders its row blocks

@@ -17,7 +17,7 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "lib", "libraytracer.so")
 
-RNG_COUNTER, RNG_REPLAY = 1, 2
+RNG_COUNTER, RNG_REPLAY, RNG_SERIAL = 1, 2, 3
 ACCEL_AUTO, ACCEL_BRUTE, ACCEL_BVH = 0, 1, 2
 FLAG_KEEP_SAMPLES = 1
 DEFAULT_SEED = 2547549
@@ -65,7 +65,7 @@ class RenderStats(C.Structure):
                 ("bvh_sphere_tests", C.c_uint64), ("bvh_node_tests", C.c_uint64),
                 ("big_sphere_tests", C.c_uint64), ("stamp_cycles", C.c_uint64 * 4),
                 ("tri_node_tests", C.c_uint64), ("bvh_tri_tests", C.c_uint64),
-                ("tri_bvh", C.c_uint32), ("fused_resolve", C.c_uint32)]
+                ("tri_bvh", C.c_uint32), ("fused_resolve", C.c_uint32), ("serial_ms", C.c_double)]
 
     def as_dict(self):
         out = {}

@@ -66,8 +66,9 @@ _Static_assert(offsetof(Rust_WorldHandle, camera) == 8, "WorldHandle.camera");
 _Static_assert(sizeof(Rust_NVec3) == 12, "NVec3");
 #include <stdio.h>
 int main(void) {
-  printf("%zu %zu %zu %zu\n", sizeof(RtRenderOptions), offsetof(RtRenderOptions, ndevices),
-         sizeof(RtRenderStats), offsetof(RtRenderStats, fused_resolve));
+  printf("%zu %zu %zu %zu %zu\n", sizeof(RtRenderOptions), offsetof(RtRenderOptions, ndevices),
+         sizeof(RtRenderStats), offsetof(RtRenderStats, fused_resolve),
+         offsetof(RtRenderStats, serial_ms));
   return 0;
 }
 """)
@@ -78,7 +79,8 @@ int main(void) {
     got = subprocess.run([str(tmp_path / "layout")], capture_output=True, text=True,
                          check=True).stdout.split()
     assert [int(x) for x in got] == [C.sizeof(R.RenderOptions), R.RenderOptions.ndevices.offset,
-                                     C.sizeof(R.RenderStats), R.RenderStats.fused_resolve.offset]
+                                     C.sizeof(R.RenderStats), R.RenderStats.fused_resolve.offset,
+                                     R.RenderStats.serial_ms.offset]
 
 
 def test_c_example_links_against_the_header():

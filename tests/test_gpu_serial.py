@@ -1,0 +1,102 @@
+"""GPU parity of RT_RNG_SERIAL: the reference's single frame-wide xorshift32
+stream (common.rs:321, random.rs:8-30) found on the device -- no replay table
+from a CPU run -- against the oracle's SERIAL mode, bit for bit.
+
+The library traces each chunk's samples from candidate stream positions,
+walks the true path through that table and renders from the start states it
+found (runtime.cpp render_frame_serial).  Cases: the
+examples/c_raytracer.rs frame (200x200, 16 spp, depth 8 -- render()'s
+settings, lib.rs:51), BASELINE configs[0] (C1), the sphere BVH (RTOW) and the
+triangle trees, edge frames, row tiles, a non-default seed, and windows forced
+too narrow so that walks fail and are resumed wider.
+"""
+import time
+
+import numpy as np
+import pytest
+
+import oracle as O
+import raytracer_amd as R
+import scenes as S
+from conftest import scene_text
+from test_gpu_parity import assert_bits_equal
+
+pytestmark = pytest.mark.gpu
+
+
+def _serial_pair(src, w, h, spp, depth, seed=R.DEFAULT_SEED, **kw):
+    img, st, _ = O.Scene(src).render(w, h, spp, depth, mode=O.RNG_SERIAL, seed=seed)
+    world = R.World(src)
+    t = time.perf_counter()
+    out, gst = world.render(w, h, spp, depth, mode=R.RNG_SERIAL, seed=seed, **kw)
+    dt = time.perf_counter() - t
+    return img, st, out, gst, dt
+
+
+@pytest.mark.parametrize("scene,w,h,spp,depth", [
+    ("c_raytracer_world.txt", 200, 200, 16, 8),  # examples/c_raytracer.rs via render()
+    ("three_spheres.txt", 256, 256, 1, 4),       # C1
+    ("world.txt", 96, 54, 8, 8),
+])
+def test_serial_frames_bit_exact(scene, w, h, spp, depth):
+    img, st, out, gst, dt = _serial_pair(scene_text(scene), w, h, spp, depth)
+    assert_bits_equal(out, img, f"{scene} SERIAL frame")
+    assert gst["rays"] == st["rays"]
+    print(f"{scene} {w}x{h}x{spp}/{depth}: start states {gst['serial_ms']:.1f} ms, "
+          f"replay trace {gst['trace_ms']:.2f} ms, call {dt * 1e3:.1f} ms")
+
+
+def test_serial_sphere_bvh_and_triangle_trees():
+    for src, accel in ((S.rtow(), R.ACCEL_BVH), (S.triangle_soup(7, 300, spheres=40, grid=6), R.ACCEL_BVH),
+                       (S.rtow(), R.ACCEL_BRUTE)):
+        img, st, out, gst, _ = _serial_pair(src, 64, 36, 4, 8, accel=accel)
+        assert_bits_equal(out, img, "SERIAL BVH frame")
+        assert gst["rays"] == st["rays"] and gst["accel"] == accel
+
+
+@pytest.mark.parametrize("w,h,spp,depth,seed", [
+    (1, 5, 3, 8, 2547549), (5, 1, 2, 8, 2547549), (6, 4, 0, 8, 2547549), (7, 3, 3, 0, 2547549),
+    (9, 7, 5, 1, 7), (33, 17, 3, 6, 123456789),
+])
+def test_serial_edge_frames(w, h, spp, depth, seed):
+    img, st, out, gst, _ = _serial_pair(scene_text("c_raytracer_world.txt"), w, h, spp, depth, seed=seed)
+    assert_bits_equal(out, img, "SERIAL edge frame")
+    assert gst["rays"] == st["rays"]
+
+
+def test_serial_windows_too_narrow_are_resumed(monkeypatch):
+    """K forced to 64 with 512-sample chunks: walks leave their windows and
+    the host resumes each failed chunk with twice the candidates."""
+    monkeypatch.setenv("RT_AMD_SERIAL_K", "64")
+    monkeypatch.setenv("RT_AMD_SERIAL_CHUNK", "512")
+    img, st, out, gst, _ = _serial_pair(scene_text("c_raytracer_world.txt"), 80, 60, 16, 8)
+    assert_bits_equal(out, img, "SERIAL frame after resumed walks")
+    monkeypatch.setenv("RT_AMD_SERIAL_CHUNK", "1")  # one sample per chunk
+    monkeypatch.setenv("RT_AMD_SERIAL_K", "1")
+    img, st, out, gst, _ = _serial_pair(scene_text("world.txt"), 12, 9, 2, 8)
+    assert_bits_equal(out, img, "SERIAL frame, one-sample chunks")
+
+
+def test_serial_tiles_are_rows_of_the_serial_frame():
+    src = scene_text("world.txt")
+    world = R.World(src)
+    full, _ = world.render(40, 30, 4, 8, mode=R.RNG_SERIAL)
+    for rank in range(3):
+        tile, _ = world.render(40, 30, 4, 8, mode=R.RNG_SERIAL, row_block=4, rank=rank, nranks=3)
+        rows = [R.tile_row(k, 4, rank, 3) for k in range(tile.shape[0])]
+        assert_bits_equal(tile, full[rows], f"SERIAL tile {rank}")
+
+
+def test_serial_after_camera_move_and_counter_frames():
+    src = scene_text("c_raytracer_world.txt")
+    world, ref = R.World(src), O.Scene(src)
+    world.render(32, 24, 4, 8)  # a COUNTER frame first (shared scratch)
+    world.move_camera(0.3, -0.2, 0.5)
+    ref.set_camera(world.camera())
+    img, _, _ = ref.render(32, 24, 4, 8, mode=O.RNG_SERIAL)
+    out, _ = world.render(32, 24, 4, 8, mode=R.RNG_SERIAL)
+    assert_bits_equal(out, img, "moved SERIAL frame")
+    cnt, _ = world.render(32, 24, 4, 8)
+    img2, _, _ = ref.render(32, 24, 4, 8, mode=O.RNG_COUNTER)
+    assert_bits_equal(cnt, img2, "COUNTER frame after SERIAL")
+    assert not np.array_equal(cnt, out)
