@@ -92,6 +92,7 @@ typedef struct RtRenderStats {
                                 (no slab, resolve_ms ~ 0)                    */
   double serial_ms;          /* RT_RNG_SERIAL: HIP-event time spent finding the
                                 start states (before the REPLAY render)       */
+  uint32_t serial_retries;   /* RT_RNG_SERIAL: chunks re-run with a wider window */
 } RtRenderStats;
 
 /* spp 16, depth 8 (lib.rs:51), COUNTER, seed 2547549, one rank, device -1,

@@ -102,28 +102,50 @@ struct TraceParams {
     const uint2 *spl;
     // SERIAL-mode passes (mode kRngSerialCount / kRngSerialEstimate): p.spp is
     // the variants per sample V and p.npix the samples of the launch; launch
-    // sample jl is sample cbase + jl of the frame (reference order, common.rs:327-336)
-    const uint32_t *win;      // kRngSerialCount: stream states from the chunk's first sample's start
-    const uint32_t *lo;       // kRngSerialCount: per chunk sample, its first candidate (B offset)
-    const uint32_t *ctrl;     // serial control block: ctrl[0] != 0 (a walk failed) -> exit at once
+    // sample jl is frame sample cbase + jl (reference order, common.rs:327-336),
+    // clamped to nserial - 1
+    const uint32_t *win;      // kRngSerialCount: stream states from sample cbase's start on
+    const double *sM;         // kRngSerialCount: prefix sums of the predicted scatter counts
+    const uint32_t *ctrl;     // serial control block (kRngSerialCount: cbase = ctrl[4];
+                              // ctrl[0] != 0, the frame is resolved: exit at once)
     uint32_t cbase;           // first frame sample of the launch
+    uint32_t nserial;         // samples in the frame
     uint32_t sspp;            // the frame's spp ...
     FastDiv div_sspp;         // ... and its divider
     uint32_t max_draws;       // 2 + 3 * max(depth, 0): bound of the draw count search
 };
 
+// Candidate k of chunk sample jl (frame sample a + jl) means B = serial_lo + k
+// scatters since sample a: the predicted offset (prefix sums M of the
+// per-sample means) minus K / 2, clamped to the possible [0, depth * jl].
+// Host, count kernel and walk kernels use this one definition.
+RT_HOST_DEVICE inline uint32_t serial_lo(const double *M, uint32_t a, uint32_t jl, uint32_t K,
+                                         uint32_t depth, uint32_t nserial) {
+    const uint32_t j = a + jl < nserial ? a + jl : nserial;
+    double c = __builtin_floor(M[j] - M[a]) - (double)(K / 2u);
+    const double hi = (double)depth * (double)jl;
+    c = c < 0.0 ? 0.0 : c;
+    c = c > hi ? hi : c;
+    return (uint32_t)c;
+}
+
 hipError_t launch_trace(const TraceParams &p, uint32_t blocks, hipStream_t stream);
-// SERIAL mode.  ctrl: u32 {fail, state at the chunk's first sample, sum of b, failing chunk}.
-// jump: 64 x 32 u32, column c of M^(2^i) (xorshift32 is linear over GF(2)).
-// Window: win[i] = xorshift32^i(ctrl[1]) for i < n.
+// SERIAL mode.  ctrl (u32[8]): {resolved, state at sample a, sum of b (low
+// bits), iterations, a = first unresolved sample, 0, iterations that stopped
+// short, 0}.  jump: 64 x 32 u32, column c of M^(2^i) (xorshift32 is linear
+// over GF(2)).  Window: win[i] = xorshift32^i(ctrl[1]) for i < n.
 hipError_t launch_serial_window(const uint32_t *ctrl, const uint32_t *jump, uint32_t *win, uint32_t n,
                                 hipStream_t stream);
-// Walk: the chunk's true path through the candidate table (b of sample jl at
-// candidate k = table[jl * K + k], plane 0 of a slab), writing each sample's
-// start state to states[jl] and the next chunk's start state to ctrl[1].
-hipError_t launch_serial_walk(uint32_t *ctrl, const float *table, const uint32_t *lo,
-                              const uint32_t *win, uint32_t *states, uint32_t nsamples, uint32_t K,
-                              uint32_t chunk, hipStream_t stream);
+// Walk: from sample a = ctrl[4], follows the true path through the candidate
+// table (b of chunk sample jl at candidate k = table[jl * K + k], plane 0 of
+// the slab) as far as it stays inside the candidate windows (at least one
+// sample), writes those samples' start states to states[a + jl] and advances
+// ctrl (a, the state at a, resolved).  bend: scratch of
+// ceil(L / serial_walk_block(L)) * K u32.
+uint32_t serial_walk_block(uint32_t L);
+hipError_t launch_serial_walk(uint32_t *ctrl, const float *table, const double *M, const uint32_t *win,
+                              uint32_t *states, uint32_t *bend, uint32_t L, uint32_t K, uint32_t depth,
+                              uint32_t nserial, hipStream_t stream);
 // inv_spp = 1.0 / (spp as f32) computed from the signed spp (common.rs:345).
 hipError_t launch_resolve_ex(const float *samples, uint32_t *out, uint32_t npix, uint32_t spp,
                              float inv_spp, uint32_t width, uint32_t slab_row0,

@@ -528,7 +528,8 @@ __device__ __forceinline__ void job_pixel(const TraceParams &p, uint32_t job, ui
     if (p.mode >= kRngSerialCount) {
         // SERIAL passes: job = launch sample * V + variant; frame sample j =
         // (row * W + col) * spp + s in the reference's loop order (common.rs:327-336)
-        const uint32_t j = p.cbase + fdiv(job, p.div_spp);
+        const uint32_t jl = fdiv(job, p.div_spp);
+        const uint32_t j = p.cbase + jl < p.nserial ? p.cbase + jl : p.nserial - 1u;
         const uint32_t pix = fdiv(j, p.div_sspp);
         s = j - pix * p.sspp;
         row = fdiv(pix, p.div_width);
@@ -549,7 +550,9 @@ __device__ __forceinline__ void job_pixel(const TraceParams &p, uint32_t job, ui
 __device__ __forceinline__ uint32_t serial_start(const TraceParams &p, uint32_t job) {
     const uint32_t jl = fdiv(job, p.div_spp);
     const uint32_t k = job - jl * p.spp;
-    if (p.mode == kRngSerialCount) return p.win[2u * jl + 3u * (p.lo[jl] + k)];
+    if (p.mode == kRngSerialCount)
+        return p.win[2u * jl + 3u * (serial_lo(p.sM, p.cbase, jl, p.spp, (p.max_draws - 2u) / 3u,
+                                               p.nserial) + k)];
     return counter_seed(p.seed, (uint64_t)(p.cbase + jl) * p.spp + k);
 }
 
@@ -685,8 +688,11 @@ template <bool kBvh, bool kLds, bool kStep, bool kMesh, bool kCount>
 __global__ __launch_bounds__(kLds ? (kMesh ? RT_LDS_BLOCK_MESH : RT_LDS_BLOCK_SPHERES) : 256)
 __attribute__((amdgpu_waves_per_eu((kMesh && !kCount) ? RT_WAVES_PER_EU_MESH : RT_WAVES_PER_EU, 8)))
 void trace_kernel(TraceParams p) {
-    // SERIAL passes: a failed walk cancels the rest of the frame's launches
-    if (p.ctrl != nullptr && p.ctrl[0] != 0u) return;
+    // SERIAL count passes: the walk of the previous pass set the first sample
+    if (p.ctrl != nullptr) {
+        if (p.ctrl[0] != 0u) return;
+        p.cbase = p.ctrl[4];  // (the walks advance it)
+    }
     const uint32_t lane = __lane_id();
     extern __shared__ float4 lds[];
     BvhView view;
@@ -1329,7 +1335,7 @@ hipError_t trace_occupancy(int *blocks_per_cu, int variant, size_t lds_bytes, bo
 // scatters of all earlier samples.  runtime.cpp render_frame_serial finds
 // every P_j chunk by chunk: trace_kernel (kRngSerialCount) traces each sample
 // of the chunk from K candidate positions around its predicted one,
-// serial_walk_kernel follows the true path through that table, and the frame
+// the walk kernels follow the true path through that table, and the frame
 // is then rendered in REPLAY mode from the start states found.
 
 // xorshift32^(2^i) as 32 columns (GF(2) matrix): y = XOR of columns c with bit c of x set
@@ -1340,53 +1346,138 @@ __device__ __forceinline__ uint32_t gf2_apply(const uint32_t *cols, uint32_t x) 
     return y;
 }
 
+// Window: thread t writes win[16t, 16t + 16): one jump to 16t (matrices of the
+// set bits), then plain xorshift steps.
+constexpr uint32_t kWinPerThread = 16;
 __global__ __launch_bounds__(256) void serial_window_kernel(const uint32_t *__restrict__ ctrl,
                                                             const uint32_t *__restrict__ jump,
                                                             uint32_t *__restrict__ win, uint32_t n) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (ctrl[0] != 0u || i >= n) return;
+    const uint32_t i0 = (blockIdx.x * blockDim.x + threadIdx.x) * kWinPerThread;
+    if (ctrl[0] != 0u || i0 >= n) return;
     uint32_t x = ctrl[1];
-    for (uint32_t b = 0; (i >> b) != 0u; ++b)
-        if ((i >> b) & 1u) x = gf2_apply(jump + 32u * b, x);
-    win[i] = x;
+    for (uint32_t b = 0; (i0 >> b) != 0u; ++b)
+        if ((i0 >> b) & 1u) x = gf2_apply(jump + 32u * b, x);
+    for (uint32_t q = 0; q < kWinPerThread && i0 + q < n; ++q) {
+        win[i0 + q] = x;
+        x ^= x << 13;
+        x ^= x >> 17;
+        x ^= x << 5;
+    }
 }
 
-__global__ __launch_bounds__(64) void serial_walk_kernel(uint32_t *__restrict__ ctrl,
-                                                         const float *__restrict__ table,
-                                                         const uint32_t *__restrict__ lo,
-                                                         const uint32_t *__restrict__ win,
-                                                         uint32_t *__restrict__ states, uint32_t nsamples,
-                                                         uint32_t K, uint32_t chunk) {
-    if (threadIdx.x != 0 || ctrl[0] != 0u) return;
-    uint32_t B = 0;  // scatters since the chunk's first sample
-    for (uint32_t jl = 0; jl < nsamples; ++jl) {
-        const uint32_t l = lo[jl];
-        const float b = (B >= l && B - l < K) ? table[(size_t)jl * K + (B - l)] : -1.0f;
-        if (!(b >= 0.0f)) {  // outside the candidate window (or no count): retry wider
-            ctrl[3] = chunk;
-            ctrl[0] = 1u;
-            return;
+// The walk through an iteration's candidate table (b of chunk sample jl at
+// candidate k = table[jl * K + k]; candidate k means B = serial_lo(jl) + k
+// scatters since sample a) in three dependent-load chains of ~32 steps
+// instead of one of L (a single-lane walk took ~0.7 ms per 2048 samples):
+//   blocks: for every block of R samples and every candidate of its first
+//     sample, follow R samples: its end offset (or ~0 if it leaves a window);
+//   finish: one lane chains the block ends from B = 0 as far as they are
+//     valid (then lane by lane inside the block where the path left its
+//     window), then one lane per block re-walks its R samples from its known
+//     start, writing start states (win[2 jl + 3 B]); ctrl advances past the
+//     resolved samples (>= 1: sample a's own window always holds B = 0).
+constexpr uint32_t kWalkInvalid = 0xFFFFFFFFu;
+__device__ __forceinline__ uint32_t walk_step(const float *table, const double *M, uint32_t a,
+                                              uint32_t K, uint32_t depth, uint32_t nserial, uint32_t jl,
+                                              uint32_t B) {
+    const uint32_t l = serial_lo(M, a, jl, K, depth, nserial);
+    const float b = (B >= l && B - l < K) ? table[(size_t)jl * K + (B - l)] : -1.0f;
+    return b >= 0.0f ? B + (uint32_t)b : kWalkInvalid;
+}
+
+__global__ __launch_bounds__(256) void serial_walk_blocks_kernel(
+    const uint32_t *__restrict__ ctrl, const float *__restrict__ table, const double *__restrict__ M,
+    uint32_t *__restrict__ bend, uint32_t L, uint32_t K, uint32_t R, uint32_t depth, uint32_t nserial) {
+    if (ctrl[0] != 0u) return;
+    const uint32_t a = ctrl[4];
+    const uint32_t n = min(L, nserial - a);
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t nb = (n + R - 1) / R;
+    if (t >= nb * K) return;
+    const uint32_t blk = t / K, k0 = t - blk * K;
+    const uint32_t j0 = blk * R, j1 = min(j0 + R, n);
+    uint32_t B = serial_lo(M, a, j0, K, depth, nserial) + k0;
+    for (uint32_t jl = j0; jl < j1 && B != kWalkInvalid; ++jl)
+        B = walk_step(table, M, a, K, depth, nserial, jl, B);
+    bend[t] = B;
+}
+
+__global__ __launch_bounds__(256) void serial_walk_finish_kernel(
+    uint32_t *__restrict__ ctrl, const float *__restrict__ table, const double *__restrict__ M,
+    const uint32_t *__restrict__ win, const uint32_t *__restrict__ bend, uint32_t *__restrict__ states,
+    uint32_t L, uint32_t K, uint32_t R, uint32_t depth, uint32_t nserial) {
+    __shared__ uint32_t bstart[256];
+    __shared__ uint32_t nfull;
+    if (ctrl[0] != 0u) return;
+    const uint32_t a = ctrl[4];
+    const uint32_t n = min(L, nserial - a);
+    const uint32_t nb = (n + R - 1) / R;
+    if (threadIdx.x == 0) {
+        uint32_t B = 0, blk = 0;
+        for (; blk < nb; ++blk) {
+            const uint32_t l = serial_lo(M, a, blk * R, K, depth, nserial);
+            const uint32_t e = (B >= l && B - l < K) ? bend[(size_t)blk * K + (B - l)] : kWalkInvalid;
+            if (e == kWalkInvalid) break;
+            bstart[blk] = B;
+            B = e;
         }
-        states[jl] = win[2u * jl + 3u * B];
-        B += (uint32_t)b;
+        nfull = blk;
+        uint32_t done = min(blk * R, n);
+        if (blk < nb) {
+            // the path leaves a window inside this block: resolve it lane-serially
+            // up to that sample (the window of the block's first sample holds B:
+            // it was the previous block's valid end, or 0)
+            const uint32_t j1 = min(blk * R + R, n);
+            for (uint32_t jl = blk * R; jl < j1; ++jl) {
+                const uint32_t nB = walk_step(table, M, a, K, depth, nserial, jl, B);
+                if (nB == kWalkInvalid) break;
+                states[a + jl] = win[2u * jl + 3u * B];
+                B = nB;
+                done = jl + 1;
+            }
+            ctrl[6] += 1u;
+        }
+        ctrl[1] = win[2u * done + 3u * B];
+        ctrl[2] += B;
+        ctrl[3] += 1u;
+        ctrl[4] = a + done;
+        if (a + done >= nserial) ctrl[0] = 1u;
     }
-    ctrl[1] = win[2u * nsamples + 3u * B];
-    ctrl[2] += B;
+    __syncthreads();
+    for (uint32_t blk = threadIdx.x; blk < nfull; blk += blockDim.x) {
+        uint32_t B = bstart[blk];
+        const uint32_t j1 = min(blk * R + R, n);
+        for (uint32_t jl = blk * R; jl < j1; ++jl) {
+            states[a + jl] = win[2u * jl + 3u * B];
+            B = walk_step(table, M, a, K, depth, nserial, jl, B);
+        }
+    }
 }
 
 hipError_t launch_serial_window(const uint32_t *ctrl, const uint32_t *jump, uint32_t *win, uint32_t n,
                                 hipStream_t stream) {
     if (!n) return hipSuccess;
-    hipLaunchKernelGGL(serial_window_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, ctrl, jump,
-                       win, n);
+    const uint32_t threads = (n + kWinPerThread - 1) / kWinPerThread;
+    hipLaunchKernelGGL(serial_window_kernel, dim3((threads + 255) / 256), dim3(256), 0, stream, ctrl,
+                       jump, win, n);
     return hipGetLastError();
 }
 
-hipError_t launch_serial_walk(uint32_t *ctrl, const float *table, const uint32_t *lo,
-                              const uint32_t *win, uint32_t *states, uint32_t nsamples, uint32_t K,
-                              uint32_t chunk, hipStream_t stream) {
-    hipLaunchKernelGGL(serial_walk_kernel, dim3(1), dim3(64), 0, stream, ctrl, table, lo, win, states,
-                       nsamples, K, chunk);
+uint32_t serial_walk_block(uint32_t L) {
+    const uint32_t R = (L + 255) / 256;
+    return R < 32u ? 32u : R;
+}
+
+hipError_t launch_serial_walk(uint32_t *ctrl, const float *table, const double *M, const uint32_t *win,
+                              uint32_t *states, uint32_t *bend, uint32_t L, uint32_t K, uint32_t depth,
+                              uint32_t nserial, hipStream_t stream) {
+    if (!L) return hipSuccess;
+    const uint32_t R = serial_walk_block(L);
+    const uint64_t nt = (uint64_t)((L + R - 1) / R) * K;
+    hipLaunchKernelGGL(serial_walk_blocks_kernel, dim3((uint32_t)((nt + 255) / 256)), dim3(256), 0, stream,
+                       ctrl, table, M, bend, L, K, R, depth, nserial);
+    hipLaunchKernelGGL(serial_walk_finish_kernel, dim3(1), dim3(256), 0, stream, ctrl, table, M, win, bend,
+                       states, L, K, R, depth, nserial);
     return hipGetLastError();
 }
 

@@ -10,6 +10,7 @@
 #include "runtime.h"
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -52,7 +53,7 @@ DeviceState::~DeviceState() {
                     bvh_nodes, bvh_prims, big_hot, bvh_miss, bvh_prim_id, big_id, bvh_miss16,
                     sph_shade, sph_kind, tbvh_nodes, tbvh_tris, tbvh_loose,
                     cam_nodes, cam_tris, ptl_off, ptl_items, spl, tile, gath,
-                    sstates, slo, swin, sjump, sctrl};
+                    sstates, sM, swin, sjump, sctrl, sbend};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
     for (hipEvent_t e : ev)
@@ -481,8 +482,9 @@ int render_frame(WorldState &w, const CameraModel &cam, size_t width, size_t hei
         p.sspp = spp;
         p.div_sspp = make_fastdiv(spp ? spp : 1);
         p.cbase = sp->cbase;
+        p.nserial = (uint32_t)((uint64_t)width * height * spp);
         p.win = sp->win;
-        p.lo = sp->lo;
+        p.sM = sp->M;
         p.ctrl = sp->ctrl;
         p.max_draws = 2u + 3u * (uint32_t)std::max(o.max_ray_bounces, 0);
         p.njobs = (uint32_t)njobs;
@@ -717,74 +719,83 @@ int render_frame_serial(WorldState &w, const CameraModel &cam, size_t width, siz
             }
         }
         const double sigma = std::sqrt(std::max(ss, 0.0) / (double)(N * R)) + 0.05;
-        // 2. chunks of L samples, K candidates per sample
+        // 2. iterations of L samples from the first unresolved one (ctrl[4]),
+        // K candidates per sample, spanning +-z sigma of the deviation of the
+        // true offset from the predicted one at the end of L samples.  Narrow
+        // windows trade progress for work: an iteration resolves samples up
+        // to where the path leaves a window, and the next one starts there
+        // with its windows re-centred (no host round trip).
         const uint64_t L = std::max<uint64_t>(1, std::min<uint64_t>(env_u64("RT_AMD_SERIAL_CHUNK", 2048), N));
+        const double z = (double)env_u64("RT_AMD_SERIAL_Z10", 20) / 10.0;
         const double spread = std::sqrt((double)L * (1.0 + 1.0 / (double)(spp * R)));
-        uint64_t K = (uint64_t)std::ceil(2.0 * 6.0 * sigma * spread) + 16;
-        if (const uint64_t k = env_u64("RT_AMD_SERIAL_K", 0)) K = k;  // (tests: force retries)
-        K = std::min<uint64_t>(std::max<uint64_t>(K, 4), (uint64_t)depth * L + 1);
-        const uint64_t nchunks = (N + L - 1) / L;
-        std::vector<uint32_t> lo(N);
-        std::vector<uint64_t> wlen(nchunks);
-        auto place = [&](uint64_t Kc) {  // candidate offsets and window lengths for K = Kc
-            for (uint64_t c = 0; c < nchunks; ++c) {
-                const uint64_t a = c * L, n = std::min<uint64_t>(L, N - a);
-                double acc = 0.0;
-                uint64_t need = 0;
-                for (uint64_t jl = 0; jl < n; ++jl) {
-                    const double centre = std::floor(acc) - (double)(Kc / 2);
-                    const double hi = (double)depth * (double)jl;
-                    const uint64_t l = (uint64_t)std::min(std::max(centre, 0.0), hi);
-                    lo[a + jl] = (uint32_t)l;
-                    need = std::max<uint64_t>(need, 2 * jl + 3 * (l + Kc));
-                    acc += mu[(a + jl) / spp];
-                }
-                wlen[c] = need + 3 * (uint64_t)depth + 3;
-            }
-        };
+        uint64_t K = (uint64_t)std::ceil(2.0 * z * sigma * spread) + 2 * (uint64_t)depth + 2;
+        if (const uint64_t k = env_u64("RT_AMD_SERIAL_K", 0)) K = k;  // (tests: narrow windows)
+        // sample a + 1's window must hold every b of sample a: K >= 2 depth + 2
+        K = std::min<uint64_t>(std::max<uint64_t>(K, 2 * (uint64_t)depth + 2), (uint64_t)depth * L + 1);
+        if (L * K > 0x7FFFFFFFull) {
+            set_error("RT_RNG_SERIAL: candidate table too large");
+            return -5;
+        }
+        // prefix sums of the predicted per-sample scatter counts
+        std::vector<double> M(N + 1);
+        M[0] = 0.0;
+        for (uint64_t j = 0; j < N; ++j) M[j + 1] = M[j] + mu[j / spp];
+        double dmax = 0.0;  // largest predicted offset within L samples: the window
+        for (uint64_t a = 0; a < N; a += std::max<uint64_t>(1, L / 4))
+            dmax = std::max(dmax, M[std::min(N, a + L + L / 4)] - M[a]);
+        const uint64_t wlen = 2 * L + 3 * ((uint64_t)std::ceil(dmax) + K + (uint64_t)depth) + 8;
+        if (wlen >= 0xFFFFFFFFull) {
+            set_error("RT_RNG_SERIAL: candidate window too large");
+            return -5;
+        }
+        const uint64_t R_walk = serial_walk_block((uint32_t)L);
+        HIP_TRY(grow(d->sM, d->sM_cap, N + 1));
+        HIP_TRY(hipMemcpyAsync(d->sM, M.data(), (N + 1) * 8, hipMemcpyHostToDevice, s));
+        HIP_TRY(grow(d->swin, d->swin_cap, wlen));
+        HIP_TRY(grow(d->sbend, d->sbend_cap, (L + R_walk - 1) / R_walk * K));
         if (!d->sjump) {
             const std::vector<uint32_t> jt = xorshift_jump_table();
             HIP_TRY(hipMalloc((void **)&d->sjump, jt.size() * 4));
             HIP_TRY(hipMemcpy(d->sjump, jt.data(), jt.size() * 4, hipMemcpyHostToDevice));
         }
-        if (!d->sctrl) HIP_TRY(hipMalloc((void **)&d->sctrl, 16));
-        HIP_TRY(grow(d->slo, d->slo_cap, N));
-        const uint32_t ctrl0[4] = {0u, o.seed, 0u, 0u};  // Random::new() state (random.rs:8-10)
-        HIP_TRY(hipMemcpyAsync(d->sctrl, ctrl0, 16, hipMemcpyHostToDevice, s));
-        uint64_t c_from = 0;
-        for (int attempt = 0;; ++attempt) {
-            place(K);
-            const uint64_t wmax = *std::max_element(wlen.begin(), wlen.end());
-            if (wmax >= 0xFFFFFFFFull || (uint64_t)L * K > 0x7FFFFFFFull) {
-                set_error("RT_RNG_SERIAL: candidate window too large");
+        if (!d->sctrl) HIP_TRY(hipMalloc((void **)&d->sctrl, 32));
+        const uint32_t ctrl0[8] = {0u, o.seed, 0u, 0u, 0u, 0u, 0u, 0u};  // Random::new() (random.rs:8-10)
+        HIP_TRY(hipMemcpyAsync(d->sctrl, ctrl0, 32, hipMemcpyHostToDevice, s));
+        // iterations are queued in batches sized by the expected progress;
+        // those queued past the end exit at once (ctrl[0])
+        uint32_t ctrl[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        double t_enqueue = 0, t_wait = 0;  // (RT_AMD_SERIAL_DEBUG)
+        uint64_t queued = 0;
+        while (!ctrl[0]) {
+            const uint64_t left = N - ctrl[4];
+            const uint64_t it = std::max<uint64_t>(2, (uint64_t)std::ceil((double)left / (0.8 * (double)L)));
+            if ((queued += it) > N + 64) {  // (every iteration resolves >= 1 sample)
+                set_error("RT_RNG_SERIAL: start states not resolved");
                 return -5;
             }
-            HIP_TRY(grow(d->swin, d->swin_cap, wmax));
-            HIP_TRY(hipMemcpyAsync(d->slo, lo.data(), N * 4, hipMemcpyHostToDevice, s));
-            for (uint64_t c = c_from; c < nchunks; ++c) {
-                const uint64_t a = c * L, n = std::min<uint64_t>(L, N - a);
-                HIP_TRY(launch_serial_window(d->sctrl, d->sjump, d->swin, (uint32_t)wlen[c], s));
-                const SerialPass sp{kRngSerialCount, (uint32_t)a, (uint32_t)n, (uint32_t)K, d->swin,
-                                    d->slo + a, d->sctrl};
+            const auto t0 = std::chrono::steady_clock::now();
+            for (uint64_t q = 0; q < it; ++q) {
+                HIP_TRY(launch_serial_window(d->sctrl, d->sjump, d->swin, (uint32_t)wlen, s));
+                const SerialPass sp{kRngSerialCount, 0u, (uint32_t)L, (uint32_t)K, d->swin, d->sM,
+                                    d->sctrl};
                 rc = render_frame(w, cam, width, height, ob, nullptr, s, nullptr, &sp);
                 if (rc) return rc;
-                HIP_TRY(launch_serial_walk(d->sctrl, d->samples, d->slo + a, d->swin, d->sstates + a,
-                                           (uint32_t)n, (uint32_t)K, (uint32_t)c, s));
+                HIP_TRY(launch_serial_walk(d->sctrl, d->samples, d->sM, d->swin, d->sstates, d->sbend,
+                                           (uint32_t)L, (uint32_t)K, depth, (uint32_t)N, s));
             }
-            uint32_t ctrl[4];
-            HIP_TRY(hipMemcpyAsync(ctrl, d->sctrl, 16, hipMemcpyDeviceToHost, s));
+            const auto t1 = std::chrono::steady_clock::now();
+            HIP_TRY(hipMemcpyAsync(ctrl, d->sctrl, 32, hipMemcpyDeviceToHost, s));
             HIP_TRY(hipStreamSynchronize(s));
-            if (ctrl[0] == 0) break;
-            // a walk left its window: resume from that chunk (its start state is
-            // still in ctrl[1]) with twice the candidates
-            if (attempt >= 6 || K >= (uint64_t)depth * L + 1) {
-                set_error("RT_RNG_SERIAL: walk left the candidate window");
-                return -5;
-            }
-            c_from = ctrl[3];
-            K = std::min<uint64_t>(2 * K, (uint64_t)depth * L + 1);
-            const uint32_t zero = 0;
-            HIP_TRY(hipMemcpyAsync(d->sctrl, &zero, 4, hipMemcpyHostToDevice, s));
+            const auto t2 = std::chrono::steady_clock::now();
+            t_enqueue += std::chrono::duration<double, std::milli>(t1 - t0).count();
+            t_wait += std::chrono::duration<double, std::milli>(t2 - t1).count();
+        }
+        if (stats) stats->serial_retries = ctrl[6];
+        if (env_u64("RT_AMD_SERIAL_DEBUG", 0)) {
+            std::fprintf(stderr, "serial debug: N %llu L %llu K %llu sigma %.3f: %u iterations (%u "
+                         "stopped short), %llu queued, enqueue %.1f ms, wait %.1f ms\n",
+                         (unsigned long long)N, (unsigned long long)L, (unsigned long long)K, sigma,
+                         ctrl[3], ctrl[6], (unsigned long long)queued, t_enqueue, t_wait);
         }
     }
     HIP_TRY(hipEventRecord(d->sev[1], s));
@@ -792,9 +803,11 @@ int render_frame_serial(WorldState &w, const CameraModel &cam, size_t width, siz
     RtRenderOptions orp = o;
     orp.rng_mode = RT_RNG_REPLAY;
     orp.replay_states = nullptr;
+    const uint32_t retries = stats ? stats->serial_retries : 0;
     rc = render_frame(w, cam, width, height, orp, d_out, s, stats, nullptr, d->sstates);
     if (rc) return rc;
     if (stats) {
+        stats->serial_retries = retries;
         float ms = 0.0f;
         HIP_TRY(hipEventSynchronize(d->sev[1]));
         HIP_TRY(hipEventElapsedTime(&ms, d->sev[0], d->sev[1]));

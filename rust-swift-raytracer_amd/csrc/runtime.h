@@ -61,8 +61,9 @@ struct DeviceState {
     // SERIAL mode (render_frame_serial): start states, candidate offsets, the
     // stream window of a chunk, xorshift jump matrices, control block
     uint32_t *sstates = nullptr;     size_t sstates_cap = 0;
-    uint32_t *slo = nullptr;         size_t slo_cap = 0;
+    double *sM = nullptr;            size_t sM_cap = 0;
     uint32_t *swin = nullptr;        size_t swin_cap = 0;
+    uint32_t *sbend = nullptr;       size_t sbend_cap = 0;
     uint32_t *sjump = nullptr;
     uint32_t *sctrl = nullptr;
     uint32_t *counter = nullptr;                                // job counter
@@ -105,7 +106,9 @@ struct WorldState {
 struct SerialPass {
     uint32_t mode;            // kRngSerialCount or kRngSerialEstimate
     uint32_t cbase, nsamples, variants;
-    const uint32_t *win, *lo, *ctrl;
+    const uint32_t *win;
+    const double *M;
+    const uint32_t *ctrl;
 };
 
 // Renders rank's tile of a width x height frame into device memory d_out

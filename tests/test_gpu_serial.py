@@ -2,13 +2,14 @@
 stream (common.rs:321, random.rs:8-30) found on the device -- no replay table
 from a CPU run -- against the oracle's SERIAL mode, bit for bit.
 
-The library traces each chunk's samples from candidate stream positions,
-walks the true path through that table and renders from the start states it
-found (runtime.cpp render_frame_serial).  Cases: the
+The library traces the next samples from candidate stream positions, walks
+the true path through that table as far as it stays inside the candidate
+windows, repeats from there, and renders from the start states it found
+(runtime.cpp render_frame_serial).  Cases: the
 examples/c_raytracer.rs frame (200x200, 16 spp, depth 8 -- render()'s
 settings, lib.rs:51), BASELINE configs[0] (C1), the sphere BVH (RTOW) and the
 triangle trees, edge frames, row tiles, a non-default seed, and windows forced
-too narrow so that walks fail and are resumed wider.
+so narrow that every iteration stops short and the next resumes there.
 """
 import time
 
@@ -64,17 +65,23 @@ def test_serial_edge_frames(w, h, spp, depth, seed):
     assert gst["rays"] == st["rays"]
 
 
-def test_serial_windows_too_narrow_are_resumed(monkeypatch):
-    """K forced to 64 with 512-sample chunks: walks leave their windows and
-    the host resumes each failed chunk with twice the candidates."""
-    monkeypatch.setenv("RT_AMD_SERIAL_K", "64")
-    monkeypatch.setenv("RT_AMD_SERIAL_CHUNK", "512")
-    img, st, out, gst, _ = _serial_pair(scene_text("c_raytracer_world.txt"), 80, 60, 16, 8)
-    assert_bits_equal(out, img, "SERIAL frame after resumed walks")
-    monkeypatch.setenv("RT_AMD_SERIAL_CHUNK", "1")  # one sample per chunk
-    monkeypatch.setenv("RT_AMD_SERIAL_K", "1")
-    img, st, out, gst, _ = _serial_pair(scene_text("world.txt"), 12, 9, 2, 8)
-    assert_bits_equal(out, img, "SERIAL frame, one-sample chunks")
+def test_serial_narrow_windows_and_short_iterations(monkeypatch):
+    """K forced to 24 candidates with 512-sample iterations: paths leave their
+    windows after a few samples and each iteration resumes where the last one
+    stopped; one-sample iterations; iterations longer than the frame."""
+    for env, scene, size in [
+        (dict(RT_AMD_SERIAL_K="24", RT_AMD_SERIAL_CHUNK="512"), "c_raytracer_world.txt", (80, 60, 16, 8)),
+        (dict(RT_AMD_SERIAL_CHUNK="1"), "world.txt", (12, 9, 2, 8)),
+        (dict(RT_AMD_SERIAL_CHUNK="100"), "world.txt", (13, 7, 3, 8)),
+        (dict(RT_AMD_SERIAL_CHUNK="100000", RT_AMD_SERIAL_Z10="5"), "world.txt", (31, 17, 4, 8)),
+    ]:
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
+        img, st, out, gst, _ = _serial_pair(scene_text(scene), *size)
+        assert_bits_equal(out, img, f"SERIAL frame {env}")
+        assert gst["rays"] == st["rays"]
+        for k in env:
+            monkeypatch.delenv(k)
 
 
 def test_serial_tiles_are_rows_of_the_serial_frame():
