@@ -95,10 +95,13 @@ typedef struct RtRenderStats {
   uint32_t serial_retries;   /* RT_RNG_SERIAL: chunks re-run with a wider window */
 } RtRenderStats;
 
-/* spp 16, depth 8 (lib.rs:51), COUNTER, seed 2547549, one rank, device -1,
- * row_block 8, ndevices 0.  render() applies the environment variable
- * RT_AMD_DEVICES=N (N >= 1) as ndevices, so a C or Swift caller of the
- * reference entry point can spread its frames over N GPUs. */
+/* spp 16, depth 8 (lib.rs:51), SERIAL, seed 2547549, one rank, device -1,
+ * row_block 8, ndevices 0: render()'s settings.  render() also reads two
+ * environment variables: RT_AMD_RNG=counter selects RT_RNG_COUNTER (fast,
+ * statistically equal frames) instead of the reference's stream, and
+ * RT_AMD_DEVICES=N (N >= 1) row-tiles its frames over N GPUs (in SERIAL mode
+ * every device finds the whole frame's start states itself: the stream is one
+ * sequential dependency, so only the REPLAY render is split). */
 void rt_default_options(RtRenderOptions *opts);
 
 /* Rows of a `height`-row image that belong to `rank` (see RtRenderOptions). */

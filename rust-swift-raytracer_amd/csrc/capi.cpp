@@ -88,6 +88,10 @@ Rust_Camera *move_camera_position(Rust_Camera *camera, float x, float y, float z
 Rust_CFramebuffer render(Rust_CFramebuffer framebuffer, const Rust_WorldHandle *handle) {
     RtRenderOptions o = reference_options();
     o.ndevices = env_devices();
+    // the reference's own frame (one xorshift32 stream, common.rs:321) unless
+    // RT_AMD_RNG=counter asks for the fast per-sample-seeded mode
+    const char *rng = std::getenv("RT_AMD_RNG");
+    if (rng && std::strcmp(rng, "counter") == 0) o.rng_mode = RT_RNG_COUNTER;
     int rc = rt_render_ex(framebuffer, handle, &o, nullptr);
     if (rc != 0) {
         std::fprintf(stderr, "raytracer render() failed (%d): %s\n", rc, rtamd::last_error().c_str());
@@ -100,7 +104,7 @@ void rt_default_options(RtRenderOptions *o) {
     std::memset(o, 0, sizeof(*o));
     o->samples_per_pixel = 16;  // lib.rs:51
     o->max_ray_bounces = 8;     // lib.rs:51
-    o->rng_mode = RT_RNG_COUNTER;
+    o->rng_mode = RT_RNG_SERIAL;  // the reference's stream (common.rs:321)
     o->seed = 2547549u;         // random.rs:9
     o->row_block = 8;  // multi-GPU tiles: blocks of 8 rows
     o->rank = 0;

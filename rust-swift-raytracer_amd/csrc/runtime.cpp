@@ -684,7 +684,7 @@ int render_frame_serial(WorldState &w, const CameraModel &cam, size_t width, siz
     if (N > 0) {
         // 1. per-pixel mean scatter counts from R counter-seeded traces per sample
         const uint64_t R = std::max<uint64_t>(
-            1, std::min<uint64_t>({(64 + spp - 1) / spp, 16, 0x7FFFFFFFull / N}));
+            1, std::min<uint64_t>({(32 + spp - 1) / spp, 16, 0x7FFFFFFFull / N}));
         const uint64_t npix = (uint64_t)width * height;
         std::vector<double> mu(npix, 0.0);
         double ss = 0.0;  // within-pixel sum of squares (sigma of one sample's b)
@@ -725,8 +725,12 @@ int render_frame_serial(WorldState &w, const CameraModel &cam, size_t width, siz
         // windows trade progress for work: an iteration resolves samples up
         // to where the path leaves a window, and the next one starts there
         // with its windows re-centred (no host round trip).
-        const uint64_t L = std::max<uint64_t>(1, std::min<uint64_t>(env_u64("RT_AMD_SERIAL_CHUNK", 2048), N));
-        const double z = (double)env_u64("RT_AMD_SERIAL_Z10", 20) / 10.0;
+        // (tools/serial_sweep.sh on the c_raytracer, C1 and RTOW frames: L 2048
+        // -> 103 / 9 / 126 ms, 4096 -> 71 / 7 / 85, 16384 -> 56 / 6 / 61, 65536 ->
+        // 72 / 6 / 64; z 1.0 / 1.5 / 2.0 within 5 %: short iterations pay the
+        // launch tail, long ones the sqrt(L) wider windows)
+        const uint64_t L = std::max<uint64_t>(1, std::min<uint64_t>(env_u64("RT_AMD_SERIAL_CHUNK", 16384), N));
+        const double z = (double)env_u64("RT_AMD_SERIAL_Z10", 15) / 10.0;
         const double spread = std::sqrt((double)L * (1.0 + 1.0 / (double)(spp * R)));
         uint64_t K = (uint64_t)std::ceil(2.0 * z * sigma * spread) + 2 * (uint64_t)depth + 2;
         if (const uint64_t k = env_u64("RT_AMD_SERIAL_K", 0)) K = k;  // (tests: narrow windows)

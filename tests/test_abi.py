@@ -96,6 +96,9 @@ def test_default_options_are_the_reference_hard_codes():
     assert (o.samples_per_pixel, o.max_ray_bounces) == (16, 8)  # lib.rs:51
     assert o.seed == 2547549 and o.rng_mode == R.RNG_COUNTER and o.nranks == 1
     assert o.ndevices == 0 and o.row_block == 8  # one device unless asked
+    raw = R.RenderOptions()
+    R.lib().rt_default_options(C.byref(raw))  # the C default: render()'s settings
+    assert raw.rng_mode == R.RNG_SERIAL and raw.samples_per_pixel == 16
 
 
 def test_counter_seed_spec_matches_oracle():

@@ -71,6 +71,7 @@ def test_render_entry_point_with_rt_amd_devices(monkeypatch):
     src = scene_text("c_raytracer_world.txt")
     img, _, _ = O.Scene(src).render(40, 30, 16, 8, mode=O.RNG_COUNTER, nthreads=8)
     world = R.World(src)
+    monkeypatch.setenv("RT_AMD_RNG", "counter")
     for v in ("1", "0", "junk"):  # 0 / invalid: one device
         monkeypatch.setenv("RT_AMD_DEVICES", v)
         assert_bits_equal(world.render_reference(40, 30), img, f"render() RT_AMD_DEVICES={v}")

@@ -112,12 +112,18 @@ def test_counter_mode_bit_exact(scene, w, h, spp, depth, seed):
     assert gst["rays"] == st["rays"]
 
 
-def test_render_abi_defaults_match_oracle_counter():
-    """render() (lib.rs:49-57 -> 16 spp, depth 8) == oracle COUNTER at 16/8."""
+def test_render_abi_defaults_match_the_reference(monkeypatch):
+    """render() (lib.rs:49-57 -> 16 spp, depth 8) == the reference's frame
+    (oracle SERIAL: one xorshift32 stream, common.rs:321), and with
+    RT_AMD_RNG=counter == oracle COUNTER at 16/8."""
     src = scene_text(CWORLD)
-    img, _, _ = O.Scene(src).render(96, 54, 16, 8, mode=O.RNG_COUNTER, nthreads=8)
+    img, _, _ = O.Scene(src).render(96, 54, 16, 8, mode=O.RNG_SERIAL)
     out = R.World(src).render_reference(96, 54)
     assert_bits_equal(out, img, "render()")
+    monkeypatch.setenv("RT_AMD_RNG", "counter")
+    img, _, _ = O.Scene(src).render(96, 54, 16, 8, mode=O.RNG_COUNTER, nthreads=8)
+    out = R.World(src).render_reference(96, 54)
+    assert_bits_equal(out, img, "render() RT_AMD_RNG=counter")
 
 
 def test_counter_vs_serial_statistics():

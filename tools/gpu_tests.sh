@@ -1,7 +1,7 @@
 #!/bin/bash
-# GPU test session: the -m gpu suite (one process, per-test time limit), then
-# a short bench.  Every GPU step has its own time limit; a crash/timeout ends
-# the session (no retries).
+# GPU test session: smoke, the -m gpu suite (one process, per-test time
+# limit), then a short bench unless NO_BENCH=1.  Every GPU step has its own
+# time limit; a crash/timeout ends the session (no retries).
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p gpurun_out
 step() {  # step <name> <seconds> <cmd...>: rc 0/1 continue, anything else stops
@@ -12,5 +12,6 @@ step() {  # step <name> <seconds> <cmd...>: rc 0/1 continue, anything else stops
     tail -5 "gpurun_out/$name.txt"
     if [ $rc -gt 1 ]; then exit $rc; fi
 }
+step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 step pytest_gpu 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread ${PYTEST_ARGS}
 [ -n "$NO_BENCH" ] || step bench 600 python bench.py --steps 5 --warmup 2
