@@ -523,9 +523,10 @@ __device__ __forceinline__ void tri_leaf(const TraceParams &p, F3 org, F3 dir, b
 // Job -> (sample, column, row): job = local pixel * spp + s (pixel-major);
 // local rows map to image rows through the rank's row blocks (tiles.py);
 // row counts from the bottom as ray_trace does (common.rs:327-331).
+template <bool kSerial>
 __device__ __forceinline__ void job_pixel(const TraceParams &p, uint32_t job, uint32_t &s,
                                           uint32_t &col, uint32_t &row) {
-    if (p.mode >= kRngSerialCount) {
+    if (kSerial) {
         // SERIAL passes: job = launch sample * V + variant; frame sample j =
         // (row * W + col) * spp + s in the reference's loop order (common.rs:327-336)
         const uint32_t jl = fdiv(job, p.div_spp);
@@ -558,11 +559,12 @@ __device__ __forceinline__ uint32_t serial_start(const TraceParams &p, uint32_t 
 
 // Primary ray against its pixel strip's candidate records (bvh.h
 // PrimaryTriLists) plus the `always` records, in any order (tri_merge).
+template <bool kSerial>
 __device__ __forceinline__ void tri_primary_list(const TraceParams &p, uint32_t job, F3 org, F3 dir,
                                                  float best_t, float &tri_t, int &tri_i,
                                                  uint32_t &tri_in, uint32_t &tri_done) {
     uint32_t s, col, row;
-    job_pixel(p, job, s, col, row);
+    job_pixel<kSerial>(p, job, s, col, row);
     const uint32_t strip = row * p.ptl_spr + col / kPrimaryTriStripW;
     const uint32_t b = p.ptl_off[strip], e = p.ptl_off[strip + 1];
     tri_done += (e - b) + (p.ptl_end - p.ptl_always);
@@ -684,12 +686,15 @@ __device__ __forceinline__ void resolve_chunk(const TraceParams &p, const float 
 #endif
 // kMesh: the scene has triangles (else the whole Mesh::hit stage compiles
 // away, which keeps the sphere-only kernel's register allocation small).
-template <bool kBvh, bool kLds, bool kStep, bool kMesh, bool kCount>
+// kSerial: the SERIAL-mode passes (render.h kRngSerial*): jobs are (sample,
+// variant) pairs and store scatter counts -- a separate instance, so the frame
+// kernels carry none of its registers.
+template <bool kBvh, bool kLds, bool kStep, bool kMesh, bool kCount, bool kSerial = false>
 __global__ __launch_bounds__(kLds ? (kMesh ? RT_LDS_BLOCK_MESH : RT_LDS_BLOCK_SPHERES) : 256)
 __attribute__((amdgpu_waves_per_eu((kMesh && !kCount) ? RT_WAVES_PER_EU_MESH : RT_WAVES_PER_EU, 8)))
 void trace_kernel(TraceParams p) {
     // SERIAL count passes: the walk of the previous pass set the first sample
-    if (p.ctrl != nullptr) {
+    if (kSerial && p.ctrl != nullptr) {
         if (p.ctrl[0] != 0u) return;
         p.cbase = p.ctrl[4];  // (the walks advance it)
     }
@@ -900,7 +905,7 @@ void trace_kernel(TraceParams p) {
                     const bool cam = bounce == 0 && p.cam_nnodes != 0;
                     if (tri_begin(p, org, dir, best_t, cam, e, tri_t, tri_i, tri_in, tri_done)) {
                         if (cam && p.ptl_off != nullptr) {
-                            tri_primary_list(p, lane_job(slot), org, dir, best_t, tri_t, tri_i, tri_in,
+                            tri_primary_list<kSerial>(p, lane_job(slot), org, dir, best_t, tri_t, tri_i, tri_in,
                                              tri_done);
                         } else {
                             node = 0;
@@ -1006,7 +1011,7 @@ void trace_kernel(TraceParams p) {
             }
             RT_STAMP(3);
             if (done) {
-                if (p.mode >= kRngSerialCount) {
+                if (kSerial) {
                     // SERIAL passes: the sample's scatter count b instead of its
                     // colour -- the draws it consumed (2 + 3b, common.rs:335-336 and
                     // random_unit_sphere per diffuse/metal scatter, common.rs:32-38)
@@ -1104,9 +1109,9 @@ void trace_kernel(TraceParams p) {
                 // states use the reference's job index below, so the
                 // enumeration order changes no bits.
                 uint32_t s, col, row;
-                job_pixel(p, job, s, col, row);
+                job_pixel<kSerial>(p, job, s, col, row);
                 slot = job + cur_off;
-                if (p.mode >= kRngSerialCount) {
+                if (kSerial) {
                     rng = serial_start(p, job);
                 } else {
                     const uint64_t gjob = ((uint64_t)row * p.width + col) * p.spp + s;
@@ -1256,37 +1261,38 @@ size_t trace_lds_bytes(const TraceParams &p) {
     return (size_t)p.nnodes * 48 + (size_t)p.nprims * 20 + (size_t)p.nsph_padded * 36;
 }
 
-template <bool kStep, bool kMesh, bool kCount>
+template <bool kStep, bool kMesh, bool kCount, bool kSerial>
 static void launch_trace_t(const TraceParams &p, uint32_t blocks, hipStream_t stream) {
     if (p.nnodes && p.use_lds)
-        hipLaunchKernelGGL((trace_kernel<true, true, kStep, kMesh, kCount>), dim3(blocks),
+        hipLaunchKernelGGL((trace_kernel<true, true, kStep, kMesh, kCount, kSerial>), dim3(blocks),
                            dim3(trace_block_threads(true, kMesh)),
                            trace_lds_bytes(p), stream, p);
     else if (p.nnodes)
-        hipLaunchKernelGGL((trace_kernel<true, false, kStep, kMesh, kCount>), dim3(blocks), dim3(256), 0,
-                           stream, p);
+        hipLaunchKernelGGL((trace_kernel<true, false, kStep, kMesh, kCount, kSerial>), dim3(blocks),
+                           dim3(256), 0, stream, p);
     else
-        hipLaunchKernelGGL((trace_kernel<false, false, kStep, kMesh, kCount>), dim3(blocks), dim3(256), 0,
-                           stream, p);
+        hipLaunchKernelGGL((trace_kernel<false, false, kStep, kMesh, kCount, kSerial>), dim3(blocks),
+                           dim3(256), 0, stream, p);
 }
 
-template <bool kCount>
+template <bool kCount, bool kSerial>
 static void launch_trace_c(const TraceParams &p, uint32_t blocks, hipStream_t stream) {
     const bool tri = p.ntri != 0;
     if (p.step) {
-        if (tri) launch_trace_t<true, true, kCount>(p, blocks, stream);
-        else launch_trace_t<true, false, kCount>(p, blocks, stream);
+        if (tri) launch_trace_t<true, true, kCount, kSerial>(p, blocks, stream);
+        else launch_trace_t<true, false, kCount, kSerial>(p, blocks, stream);
     } else {
-        if (tri) launch_trace_t<false, true, kCount>(p, blocks, stream);
-        else launch_trace_t<false, false, kCount>(p, blocks, stream);
+        if (tri) launch_trace_t<false, true, kCount, kSerial>(p, blocks, stream);
+        else launch_trace_t<false, false, kCount, kSerial>(p, blocks, stream);
     }
 }
 
 // Frames rendered without stats run a variant whose work counters compile away
-// (one VALU increment per node / sphere test / ray).
+// (one VALU increment per node / sphere test / ray); SERIAL passes their own.
 hipError_t launch_trace(const TraceParams &p, uint32_t blocks, hipStream_t stream) {
-    if (p.stats) launch_trace_c<true>(p, blocks, stream);
-    else launch_trace_c<false>(p, blocks, stream);
+    if (p.mode >= kRngSerialCount) launch_trace_c<false, true>(p, blocks, stream);
+    else if (p.stats) launch_trace_c<true, false>(p, blocks, stream);
+    else launch_trace_c<false, false>(p, blocks, stream);
     return hipGetLastError();
 }
 
