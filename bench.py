@@ -176,6 +176,37 @@ def _timed(args, step, stream, sync, barrier):
     return st_warm, stats[-1], elapsed, trace_ms, count_trace_ms
 
 
+def _post_move(world, step, sync, dz=-0.05):
+    """Interactive re-render (lib.rs:60-63, GameView.swift:198-219): the frame
+    right after move_camera_position, against steady frames of the moved
+    camera.  The moved camera's primary candidate lists / camera tree are
+    built on a host thread meanwhile; the first frame renders without them."""
+    sync()
+    world.move_camera(0.0, 0.0, dz)
+    t0 = time.perf_counter()
+    st = step(True)  # (with counters: the flags say what the frame used)
+    sync()
+    first = (time.perf_counter() - t0) * 1e3
+    first_lists = int(st["primary_lists"] or st["camera_tree"])
+    t0 = time.perf_counter()
+    while not (st["primary_lists"] or st["camera_tree"]) and time.perf_counter() - t0 < 10:
+        time.sleep(0.002)
+        st = step(True)
+    ready = (time.perf_counter() - t0) * 1e3
+    sync()
+    times = []
+    for _ in range(5):
+        t = time.perf_counter()
+        step(True)
+        sync()
+        times.append((time.perf_counter() - t) * 1e3)
+    steady = sorted(times)[len(times) // 2]
+    return {"move": [0.0, 0.0, dz], "first_frame_ms": first, "steady_frame_ms": steady,
+            "ratio": first / steady, "lists_ready_ms": ready,
+            "first_frame_lists": first_lists,
+            "steady_lists": int(st["primary_lists"] or st["camera_tree"])}
+
+
 def single_process(args):
     """N GPUs from this one process through the library's multi-device mode
     (RtRenderOptions.ndevices): every device renders its row blocks, an RCCL
@@ -209,11 +240,13 @@ def single_process(args):
             torch.cuda.synchronize(d)
 
     st_warm, st0, elapsed, trace_ms, count_trace_ms = _timed(args, step, stream, sync, lambda: None)
+    moved = _post_move(world, step, sync)
     rows = R.tile_rows(H, ROW_BLOCK, 0, ngpu) if ngpu > 1 else H
     par = (f"row-tiles x{ngpu} (block {ROW_BLOCK}), one process, RCCL ncclGather "
            f"({ranks} ranks) to device 0")
     _report(args, src, world, W, H, spp, depth, st0, st_warm["rays"] * args.steps, elapsed,
-            trace_ms, count_trace_ms, ngpu, rows, par, {"rccl_ranks": ranks, "launch": "single process"})
+            trace_ms, count_trace_ms, ngpu, rows, par,
+            {"rccl_ranks": ranks, "launch": "single process", "post_move": moved})
 
 
 def multi_process(args, world_size):

@@ -92,7 +92,12 @@ typedef struct RtRenderStats {
                                 (no slab, resolve_ms ~ 0)                    */
   double serial_ms;          /* RT_RNG_SERIAL: HIP-event time spent finding the
                                 start states (before the REPLAY render)       */
-  uint32_t serial_retries;   /* RT_RNG_SERIAL: chunks re-run with a wider window */
+  uint32_t serial_retries;   /* RT_RNG_SERIAL: iterations whose walk stopped
+                                short of their samples (the next one resumed) */
+  uint32_t primary_lists;    /* 1: primary rays used per-pixel / per-strip
+                                candidate lists (0 right after a camera move or
+                                resize while they are built on a host thread) */
+  uint32_t camera_tree;      /* 1: bounce-0 triangle rays used the camera tree */
 } RtRenderStats;
 
 /* spp 16, depth 8 (lib.rs:51), SERIAL, seed 2547549, one rank, device -1,

@@ -200,41 +200,115 @@ static int device_for(WorldState &w, int want, DeviceState *&out) {
     return 0;
 }
 
+static uint32_t cam_leaf() {
+    return (uint32_t)env_u64("RT_AMD_CAM_LEAF", 2);  // triangles per camera-tree leaf
+}
+
 void prepare_camera(WorldState &w, const CameraModel &cam) {
     if (w.tbvh.nodes.empty() || env_u64("RT_AMD_CAMERA_TREE", 1) == 0) return;
     const float o[3] = {cam.origin.x, cam.origin.y, cam.origin.z};
     if (w.ctree_version && std::memcmp(o, w.ctree.origin, sizeof(o)) == 0) return;
-    const uint64_t leaf = env_u64("RT_AMD_CAM_LEAF", 2);  // triangles per camera-tree leaf
-    w.ctree = build_camera_triangle_bvh(w.scene.triangles, w.packed.tri_hot, w.tbvh, o,
-                                        (uint32_t)leaf);
+    w.ctree = build_camera_triangle_bvh(w.scene.triangles, w.packed.tri_hot, w.tbvh, o, cam_leaf());
     ++w.ctree_version;
 }
 
-// Primary-ray triangle lists for this camera and frame size (bvh.h); rebuilt
-// when either (or the camera tree) changes: ~22 ms at C5 on one host core.
-static void prepare_primary_tri_lists(WorldState &w, const CameraModel &cam, size_t width,
-                                      size_t height) {
-    if (w.ptl_version && w.ptl_w == width && w.ptl_h == height && w.ptl_ctree == w.ctree_version &&
-        std::memcmp(&w.ptl_cam, &cam, sizeof(cam)) == 0)
-        return;
-    w.ptl = build_primary_tri_lists(w.ctree, cam, width, height);
-    w.ptl_cam = cam;
-    w.ptl_w = width;
-    w.ptl_h = height;
-    w.ptl_ctree = w.ctree_version;
-    ++w.ptl_version;
+// Host structures for a new camera or frame size are built on a host thread
+// while frames render without them (RT_AMD_SYNC_LISTS=1: built before the
+// frame, as load_world does for its camera).  Every frame is bit-identical
+// either way; only the work per primary ray differs.
+static bool sync_lists() { return env_u64("RT_AMD_SYNC_LISTS", 0) != 0; }
+
+template <typename T>
+static bool job_ready(const std::future<T> &f) {
+    return f.valid() && f.wait_for(std::chrono::seconds(0)) == std::future_status::ready;
 }
 
-static void prepare_primary_sphere_lists(WorldState &w, const CameraModel &cam, size_t width,
+static bool same_cam(const CameraModel &a, const CameraModel &b) {
+    return std::memcmp(&a, &b, sizeof(a)) == 0;
+}
+
+// Camera tree (bounce-0 triangle tree for the camera origin) and the primary
+// strip lists (~0.2 s + 22 ms at C5 on one host core).  Returns true when both
+// are current for (cam, width, height); false: this frame walks the static tree.
+static bool prepare_camera_lists(WorldState &w, const CameraModel &cam, size_t width, size_t height,
+                                 bool lists) {
+    if (w.tbvh.nodes.empty() || env_u64("RT_AMD_CAMERA_TREE", 1) == 0) return false;
+    const bool tree_ok = w.ctree_version && std::memcmp(&cam.origin, w.ctree.origin, 12) == 0;
+    const bool lists_ok = !lists || (w.ptl_version && w.ptl_w == width && w.ptl_h == height &&
+                                     w.ptl_ctree == w.ctree_version && same_cam(w.ptl_cam, cam));
+    if (tree_ok && lists_ok) return true;
+    if (sync_lists() || (tree_ok && !lists_ok)) {
+        // (a frame-size change keeps the tree: the lists alone take ~22 ms)
+        prepare_camera(w, cam);
+        if (lists) {
+            w.ptl = build_primary_tri_lists(w.ctree, cam, width, height);
+            w.ptl_cam = cam;
+            w.ptl_w = width;
+            w.ptl_h = height;
+            w.ptl_ctree = w.ctree_version;
+            ++w.ptl_version;
+        }
+        return true;
+    }
+    WorldState::CamJob &j = w.cam_job;
+    if (j.f.valid()) {
+        if (!job_ready(j.f)) return false;  // (one build at a time)
+        auto built = j.f.get();
+        if (same_cam(j.cam, cam) && j.w == width && j.h == height) {
+            w.ctree = std::move(built.first);
+            ++w.ctree_version;
+            w.ptl = std::move(built.second);
+            w.ptl_cam = cam;
+            w.ptl_w = width;
+            w.ptl_h = height;
+            w.ptl_ctree = w.ctree_version;
+            ++w.ptl_version;
+            return true;
+        }
+    }
+    j.cam = cam;
+    j.w = width;
+    j.h = height;
+    const uint32_t leaf = cam_leaf();
+    j.f = std::async(std::launch::async, [&w, cam, width, height, lists, leaf]() {
+        const float o[3] = {cam.origin.x, cam.origin.y, cam.origin.z};
+        std::pair<CameraTriangleBVH, PrimaryTriLists> r;
+        r.first = build_camera_triangle_bvh(w.scene.triangles, w.packed.tri_hot, w.tbvh, o, leaf);
+        if (lists) r.second = build_primary_tri_lists(r.first, cam, width, height);
+        return r;
+    });
+    return false;
+}
+
+// Primary sphere candidates per pixel (< 50 ms at 1080p on one host core).
+// Returns true when w.spl is current for (cam, width, height).
+static bool prepare_primary_sphere_lists(WorldState &w, const CameraModel &cam, size_t width,
                                          size_t height) {
-    if (w.spl_version && w.spl_w == width && w.spl_h == height &&
-        std::memcmp(&w.spl_cam, &cam, sizeof(cam)) == 0)
-        return;
-    w.spl = build_primary_sphere_lists(w.bvh, cam, width, height);
+    if (w.spl_version && w.spl_w == width && w.spl_h == height && same_cam(w.spl_cam, cam))
+        return true;
+    WorldState::SplJob &j = w.spl_job;
+    if (sync_lists()) {
+        w.spl = build_primary_sphere_lists(w.bvh, cam, width, height);
+    } else {
+        if (j.f.valid() && !job_ready(j.f)) return false;  // (one build at a time)
+        if (j.f.valid() && same_cam(j.cam, cam) && j.w == width && j.h == height) {
+            w.spl = j.f.get();
+        } else {
+            if (j.f.valid()) (void)j.f.get();  // a finished build for another camera
+            j.cam = cam;
+            j.w = width;
+            j.h = height;
+            j.f = std::async(std::launch::async, [&w, cam, width, height]() {
+                return build_primary_sphere_lists(w.bvh, cam, width, height);
+            });
+            return false;
+        }
+    }
     w.spl_cam = cam;
     w.spl_w = width;
     w.spl_h = height;
     ++w.spl_version;
+    return true;
 }
 
 template <typename T>
@@ -304,6 +378,7 @@ int render_frame(WorldState &w, const CameraModel &cam, size_t width, size_t hei
     }
 
     TraceParams p{};
+    bool primary_lists = false;  // the frame's primary rays use candidate lists
     p.sph_hot = d->sph_hot; p.sph_cold = d->sph_cold;
     p.tri_hot = d->tri_hot; p.tri_geo = d->tri_geo;
     p.mats = d->mats;
@@ -350,8 +425,8 @@ int render_frame(WorldState &w, const CameraModel &cam, size_t width, size_t hei
         p.bvh_r = bv.radius; p.bvh_rmax = bv.rmax; p.bvh_mag = bv.mag;
         p.bvh_inv_rmin = env_u64("RT_AMD_LINEAR_E", 0) ? INFINITY : bv.inv_rmin;
         // sphere-only scenes: primary rays test their pixel's candidates
-        if (d->ntri == 0 && env_u64("RT_AMD_SPHERE_LISTS", 1) != 0) {
-            prepare_primary_sphere_lists(w, cam, width, height);
+        if (d->ntri == 0 && env_u64("RT_AMD_SPHERE_LISTS", 1) != 0 &&
+            prepare_primary_sphere_lists(w, cam, width, height)) {
             if (d->spl_version != w.spl_version) {
                 if (d->spl) HIP_TRY(hipFree(d->spl));
                 d->spl = nullptr;
@@ -363,10 +438,12 @@ int render_frame(WorldState &w, const CameraModel &cam, size_t width, size_t hei
                 d->spl_version = w.spl_version;
             }
             p.spl = d->spl;
+            primary_lists = p.spl != nullptr;
         }
     }
     const bool use_tbvh = d->tnodes > 0 && o.accel != RT_ACCEL_BRUTE;
-    if (use_tbvh) prepare_camera(w, cam);
+    const bool want_ptl = width >= 2 && height >= 2 && env_u64("RT_AMD_PRIMARY_LISTS", 1) != 0;
+    if (use_tbvh) prepare_camera_lists(w, cam, width, height, want_ptl);
     if (use_tbvh && w.ctree_version && d->cam_version != w.ctree_version) {
         for (void *b : {(void *)d->cam_nodes, (void *)d->cam_tris})
             if (b) HIP_TRY(hipFree(b));
@@ -387,8 +464,8 @@ int render_frame(WorldState &w, const CameraModel &cam, size_t width, size_t hei
         if (d->cam_nnodes && std::memcmp(w.ctree.origin, &cam.origin, 12) == 0) {
             p.cam_nodes = d->cam_nodes; p.cam_tris = d->cam_tris;
             p.cam_nnodes = d->cam_nnodes;
-            if (width >= 2 && height >= 2 && env_u64("RT_AMD_PRIMARY_LISTS", 1) != 0) {
-                prepare_primary_tri_lists(w, cam, width, height);
+            if (want_ptl && w.ptl_version && w.ptl_w == width && w.ptl_h == height &&
+                w.ptl_ctree == w.ctree_version && same_cam(w.ptl_cam, cam)) {
                 if (d->ptl_version != w.ptl_version) {
                     for (void *b : {(void *)d->ptl_off, (void *)d->ptl_items})
                         if (b) HIP_TRY(hipFree(b));
@@ -406,6 +483,7 @@ int render_frame(WorldState &w, const CameraModel &cam, size_t width, size_t hei
                     d->ptl_version = w.ptl_version;
                 }
                 if (d->ptl_off) {
+                    primary_lists = true;
                     p.ptl_off = d->ptl_off;
                     p.ptl_items = d->ptl_items;
                     p.ptl_spr = w.ptl.strips_per_row;
@@ -604,6 +682,8 @@ int render_frame(WorldState &w, const CameraModel &cam, size_t width, size_t hei
         stats->tri_node_tests = st[8];
         stats->tri_bvh = use_tbvh ? 1u : 0u;
         stats->fused_resolve = fused ? 1u : 0u;
+        stats->primary_lists = primary_lists ? 1u : 0u;
+        stats->camera_tree = p.cam_nnodes != 0 ? 1u : 0u;
         stats->bvh_tri_tests = use_tbvh ? st[9] : stats->tri_tests;
     }
     return 0;
@@ -965,6 +1045,7 @@ int render_frame_multi(WorldState &w, const CameraModel &cam, size_t width, size
             for (int k = 0; k < 4; ++k) stats->stamp_cycles[k] += sg.stamp_cycles[k];
             stats->tri_node_tests += sg.tri_node_tests; stats->bvh_tri_tests += sg.bvh_tri_tests;
             stats->tri_bvh = sg.tri_bvh; stats->fused_resolve = sg.fused_resolve;
+            stats->primary_lists = sg.primary_lists; stats->camera_tree = sg.camera_tree;
         }
     }
     // RCCL gather of equal-size tiles to the first device (over xGMI); with one

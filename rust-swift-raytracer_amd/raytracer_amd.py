@@ -66,7 +66,8 @@ class RenderStats(C.Structure):
                 ("big_sphere_tests", C.c_uint64), ("stamp_cycles", C.c_uint64 * 4),
                 ("tri_node_tests", C.c_uint64), ("bvh_tri_tests", C.c_uint64),
                 ("tri_bvh", C.c_uint32), ("fused_resolve", C.c_uint32), ("serial_ms", C.c_double),
-                ("serial_retries", C.c_uint32)]
+                ("serial_retries", C.c_uint32), ("primary_lists", C.c_uint32),
+                ("camera_tree", C.c_uint32)]
 
     def as_dict(self):
         out = {}

@@ -389,6 +389,7 @@ def test_primary_sphere_lists_follow_camera_and_size(monkeypatch):
     frame size (bvh.h PrimarySphereLists): after camera moves (one into the
     sphere field, one far off, which falls back to the walk) and at several
     sizes every sample equals the tree walk's and brute force."""
+    monkeypatch.setenv("RT_AMD_SYNC_LISTS", "1")  # lists built before each frame
     src = S.rtow()
     world = R.World(src)
     for mv, (w, h) in [((0.0, 0.0, 0.0), (96, 54)), ((0.0, 0.0, 0.0), (57, 31)),
@@ -407,6 +408,7 @@ def test_primary_sphere_lists_follow_camera_and_size(monkeypatch):
         assert_bits_equal(sb_[:, :3], sa[:, :3], f"samples (lists) {mv} {w}x{h}")
         assert_bits_equal(sc_[:, :3], sa[:, :3], f"samples (walk) {mv} {w}x{h}")
         assert sb["rays"] == sc["rays"]
+        assert sb["primary_lists"] == (1 if abs(mv[2]) < 1000 else 0) and sc["primary_lists"] == 0
 
 
 def test_bvh_full_size_c2_equals_brute_force():
@@ -461,9 +463,10 @@ def test_triangle_bvh_c5_equals_brute_force():
     assert sa["rays"] == sb["rays"]
 
 
-def test_triangle_camera_tree_follows_camera_moves():
+def test_triangle_camera_tree_follows_camera_moves(monkeypatch):
     """Bounce-0 rays use a tree built for the camera origin; moving the camera
     must rebuild it (every sample still equals brute force)."""
+    monkeypatch.setenv("RT_AMD_SYNC_LISTS", "1")  # tree built before each frame
     src = _triangle_scene(31, 500, size=1.0, spheres=30, grid=10)
     world = R.World(src)
     for mv in [(0.0, 0.0, 0.0), (0.5, -0.25, 1.0), (-3.0, 2.0, -4.0), (0.0, 0.0, 0.0)]:
@@ -472,16 +475,17 @@ def test_triangle_camera_tree_follows_camera_moves():
         sma = world.read_samples(64 * 48 * 4)
         b, sb = render_kept(world, 64, 48, 4, 8, accel=R.ACCEL_BVH)
         smb = world.read_samples(64 * 48 * 4)
-        assert sb["tri_bvh"] == 1
+        assert sb["tri_bvh"] == 1 and sb["camera_tree"] == 1
         assert_bits_equal(b, a, f"frame after move {mv}")
         assert_bits_equal(smb[:, :3], sma[:, :3], f"samples after move {mv}")
 
 
-def test_primary_triangle_lists_follow_camera_and_size():
+def test_primary_triangle_lists_follow_camera_and_size(monkeypatch):
     """Bounce-0 rays test per-strip candidate lists built for the camera and
     the frame size: after every move and at every size each sample equals
     brute force (includes a camera inside the soup and one looking at the
     soup from behind)."""
+    monkeypatch.setenv("RT_AMD_SYNC_LISTS", "1")  # lists built before each frame
     src = _triangle_scene(51, 600, size=0.8, spheres=30, grid=8)
     world = R.World(src)
     for mv, (w, h) in [((0.0, 0.0, 0.0), (128, 72)), ((0.0, 0.0, 0.0), (97, 61)),
@@ -492,7 +496,7 @@ def test_primary_triangle_lists_follow_camera_and_size():
         sa = world.read_samples(w * h * 4)
         b, sb = render_kept(world, w, h, 4, 8, accel=R.ACCEL_BVH)
         smb = world.read_samples(w * h * 4)
-        assert sb["tri_bvh"] == 1
+        assert sb["tri_bvh"] == 1 and sb["camera_tree"] == 1 and sb["primary_lists"] == 1
         assert_bits_equal(b, a, f"frame {mv} {w}x{h}")
         assert_bits_equal(smb[:, :3], sa[:, :3], f"samples {mv} {w}x{h}")
 
@@ -506,3 +510,30 @@ def test_triangle_bvh_edge_frames(w, h, spp, depth):
     out, gst = R.World(src).render(w, h, spp, depth)
     assert_bits_equal(out, img, "edge frame")
     assert gst["rays"] == st["rays"]
+
+
+@pytest.mark.parametrize("scene", ["rtow", "mesh_soup"])
+def test_lists_built_in_the_background_after_camera_moves(scene):
+    """After a camera move (or on a new world) the first frames render without
+    the primary candidate lists / camera tree while a host thread builds them
+    (interactive re-render, lib.rs:60-63); the frames after the build use
+    them.  Every frame equals brute force."""
+    import time
+
+    src = S.rtow() if scene == "rtow" else _triangle_scene(31, 500, size=1.0, spheres=30, grid=10)
+    flag = "primary_lists" if scene == "rtow" else "camera_tree"
+    world = R.World(src)
+    w, h, spp = 96, 54, 2
+    for mv in [(0.0, 0.0, 0.0), (0.4, -0.3, -2.0), (-1.0, 0.5, 3.0)]:
+        world.move_camera(*mv)
+        ref, _ = world.render(w, h, spp, 8, accel=R.ACCEL_BRUTE)
+        out, st = world.render(w, h, spp, 8)
+        assert_bits_equal(out, ref, f"first frame after {mv}")
+        if mv != (0.0, 0.0, 0.0) or scene == "rtow":
+            assert st[flag] == 0  # the build has just been started
+        deadline = time.time() + 30
+        while st[flag] == 0 and time.time() < deadline:
+            time.sleep(0.005)
+            out, st = world.render(w, h, spp, 8)
+            assert_bits_equal(out, ref, f"frame during the build after {mv}")
+        assert st[flag] == 1, f"lists never adopted after {mv}"
