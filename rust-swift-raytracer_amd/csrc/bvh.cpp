@@ -2,10 +2,12 @@
 #include "bvh.h"
 
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
 #include <limits>
+#include <thread>
 
 namespace rtamd {
 
@@ -55,6 +57,53 @@ struct Builder {
 
     Builder(std::vector<Prim> &p, uint32_t ls, double ph = 0) : prims(p), leaf_size(ls), phantom(ph) {}
 
+    // Subtrees of at least kParMin prims below depth kParDepth are built on
+    // their own threads (they partition disjoint prim ranges) and spliced in
+    // afterwards: the same splits as a serial build, only node numbering
+    // differs (which no result depends on, bvh.h).  C5's camera tree: 263 ->
+    // ~45 ms on 16 threads.
+    static constexpr uint32_t kParDepth = 4, kParMin = 512;
+    struct Task { uint32_t n, first, count, depth; };
+    std::vector<Task> deferred;
+    bool defer = false;
+
+    void build_root(uint32_t count) {
+        nodes.reserve((size_t)count * 2);
+        nodes.emplace_back();
+        unsigned hw = std::thread::hardware_concurrency();
+        const unsigned threads = std::min(16u, std::max(1u, hw));
+        defer = threads > 1 && count >= 4 * kParMin;
+        build(0, 0, count, 0);
+        defer = false;
+        if (deferred.empty()) return;
+        std::vector<Builder> sub(deferred.size(), Builder(prims, leaf_size, phantom));
+        std::atomic<size_t> next{0};
+        auto work = [&]() {
+            for (size_t t; (t = next.fetch_add(1)) < deferred.size();) {
+                const Task &k = deferred[t];
+                sub[t].nodes.reserve((size_t)k.count * 2);
+                sub[t].nodes.emplace_back();
+                sub[t].build(0, k.first, k.count, k.depth);
+            }
+        };
+        std::vector<std::thread> pool;
+        for (unsigned i = 1; i < std::min<size_t>(threads, deferred.size()); ++i) pool.emplace_back(work);
+        work();
+        for (auto &t : pool) t.join();
+        for (size_t t = 0; t < deferred.size(); ++t) {
+            // local node 0 becomes the placeholder n, local i > 0 lands at base + i - 1
+            const uint32_t base = (uint32_t)nodes.size();
+            auto remap = [&](Node nd) {
+                if (!nd.leaf) nd.a = base + nd.a - 1;  // children are never a local root
+                return nd;
+            };
+            nodes[deferred[t].n] = remap(sub[t].nodes[0]);
+            for (size_t i = 1; i < sub[t].nodes.size(); ++i) nodes.push_back(remap(sub[t].nodes[i]));
+            max_depth = std::max(max_depth, sub[t].max_depth);
+        }
+        deferred.clear();
+    }
+
     double cost_area(const Box &g, const Box &n) const {
         if (phantom <= 0) return g.area();
         double dn[3], sum = 0, e[3];
@@ -75,6 +124,10 @@ struct Builder {
 
     // Builds node n over prims[first, first + count).
     void build(uint32_t n, uint32_t first, uint32_t count, uint32_t depth) {
+        if (defer && depth == kParDepth && count >= kParMin) {
+            deferred.push_back({n, first, count, depth});
+            return;
+        }
         max_depth = std::max(max_depth, depth);
         Box box, cbox, nbox;
         for (uint32_t i = first; i < first + count; ++i) {
@@ -399,9 +452,7 @@ TriangleBVH build_triangle_bvh(const std::vector<Triangle> &tris, const std::vec
     if (const char *e = std::getenv("RT_AMD_TRI_PHANTOM")) L = std::atof(e);
     if (phantom > 0) L = phantom;
     Builder b(prims, std::min(7u, std::max(1u, leaf_size)), L > 0 ? L : 1e-30);  // count: 3 bits
-    b.nodes.reserve(prims.size() * 2);
-    b.nodes.emplace_back();
-    b.build(0, 0, (uint32_t)prims.size(), 0);
+    b.build_root((uint32_t)prims.size());
     out.depth = b.max_depth;
     std::vector<Box> nbox(b.nodes.size());
     normal_boxes(b, prims, 0, nbox);
@@ -469,9 +520,7 @@ CameraTriangleBVH build_camera_triangle_bvh(const std::vector<Triangle> &tris,
     }
     if (prims.empty()) return out;
     Builder b(prims, std::min(7u, std::max(1u, leaf_size)));  // count: 3 bits
-    b.nodes.reserve(prims.size() * 2);
-    b.nodes.emplace_back();
-    b.build(0, 0, (uint32_t)prims.size(), 0);
+    b.build_root((uint32_t)prims.size());
     out.depth = b.max_depth;
     out.nodes.resize(b.nodes.size() * 8);
     for (size_t n = 0; n < b.nodes.size(); ++n) {
@@ -531,9 +580,7 @@ SphereBVH build_sphere_bvh(const std::vector<Sphere> &spheres, uint32_t leaf_siz
         return out;
     }
     Builder b(prims, std::max(1u, leaf_size));
-    b.nodes.reserve(prims.size() * 2);
-    b.nodes.emplace_back();
-    b.build(0, 0, (uint32_t)prims.size(), 0);
+    b.build_root((uint32_t)prims.size());
     out.depth = b.max_depth;
 
     Box all;

@@ -212,10 +212,10 @@ void prepare_camera(WorldState &w, const CameraModel &cam) {
     ++w.ctree_version;
 }
 
-// Host structures for a new camera or frame size are built on a host thread
-// while frames render without them (RT_AMD_SYNC_LISTS=1: built before the
-// frame, as load_world does for its camera).  Every frame is bit-identical
-// either way; only the work per primary ray differs.
+// Primary sphere lists for a new camera or frame size are built on a host
+// thread while frames render without them (RT_AMD_SYNC_LISTS=1: built before
+// the frame).  Every frame is bit-identical either way; only the work per
+// primary ray differs (C2: +3 % per frame without them).
 static bool sync_lists() { return env_u64("RT_AMD_SYNC_LISTS", 0) != 0; }
 
 template <typename T>
@@ -228,56 +228,23 @@ static bool same_cam(const CameraModel &a, const CameraModel &b) {
 }
 
 // Camera tree (bounce-0 triangle tree for the camera origin) and the primary
-// strip lists (~0.2 s + 22 ms at C5 on one host core).  Returns true when both
-// are current for (cam, width, height); false: this frame walks the static tree.
-static bool prepare_camera_lists(WorldState &w, const CameraModel &cam, size_t width, size_t height,
+// strip lists for (cam, width, height), rebuilt before the frame when either
+// changed.  Unlike the sphere lists these are not deferred to a host thread:
+// a C5 frame without them costs ~660 ms instead of ~221 ms, while the
+// rebuild takes ~50 + 6 ms (subtrees built on 16 host threads, bvh.cpp).
+static void prepare_camera_lists(WorldState &w, const CameraModel &cam, size_t width, size_t height,
                                  bool lists) {
-    if (w.tbvh.nodes.empty() || env_u64("RT_AMD_CAMERA_TREE", 1) == 0) return false;
-    const bool tree_ok = w.ctree_version && std::memcmp(&cam.origin, w.ctree.origin, 12) == 0;
-    const bool lists_ok = !lists || (w.ptl_version && w.ptl_w == width && w.ptl_h == height &&
-                                     w.ptl_ctree == w.ctree_version && same_cam(w.ptl_cam, cam));
-    if (tree_ok && lists_ok) return true;
-    if (sync_lists() || (tree_ok && !lists_ok)) {
-        // (a frame-size change keeps the tree: the lists alone take ~22 ms)
-        prepare_camera(w, cam);
-        if (lists) {
-            w.ptl = build_primary_tri_lists(w.ctree, cam, width, height);
-            w.ptl_cam = cam;
-            w.ptl_w = width;
-            w.ptl_h = height;
-            w.ptl_ctree = w.ctree_version;
-            ++w.ptl_version;
-        }
-        return true;
-    }
-    WorldState::CamJob &j = w.cam_job;
-    if (j.f.valid()) {
-        if (!job_ready(j.f)) return false;  // (one build at a time)
-        auto built = j.f.get();
-        if (same_cam(j.cam, cam) && j.w == width && j.h == height) {
-            w.ctree = std::move(built.first);
-            ++w.ctree_version;
-            w.ptl = std::move(built.second);
-            w.ptl_cam = cam;
-            w.ptl_w = width;
-            w.ptl_h = height;
-            w.ptl_ctree = w.ctree_version;
-            ++w.ptl_version;
-            return true;
-        }
-    }
-    j.cam = cam;
-    j.w = width;
-    j.h = height;
-    const uint32_t leaf = cam_leaf();
-    j.f = std::async(std::launch::async, [&w, cam, width, height, lists, leaf]() {
-        const float o[3] = {cam.origin.x, cam.origin.y, cam.origin.z};
-        std::pair<CameraTriangleBVH, PrimaryTriLists> r;
-        r.first = build_camera_triangle_bvh(w.scene.triangles, w.packed.tri_hot, w.tbvh, o, leaf);
-        if (lists) r.second = build_primary_tri_lists(r.first, cam, width, height);
-        return r;
-    });
-    return false;
+    prepare_camera(w, cam);
+    if (!lists || !w.ctree_version) return;
+    if (w.ptl_version && w.ptl_w == width && w.ptl_h == height && w.ptl_ctree == w.ctree_version &&
+        same_cam(w.ptl_cam, cam))
+        return;
+    w.ptl = build_primary_tri_lists(w.ctree, cam, width, height);
+    w.ptl_cam = cam;
+    w.ptl_w = width;
+    w.ptl_h = height;
+    w.ptl_ctree = w.ctree_version;
+    ++w.ptl_version;
 }
 
 // Primary sphere candidates per pixel (< 50 ms at 1080p on one host core).

@@ -7,7 +7,6 @@
 #include <future>
 #include <map>
 #include <mutex>
-#include <utility>
 #include <memory>
 #include <string>
 
@@ -95,17 +94,12 @@ struct WorldState {
     CameraModel spl_cam{};
     size_t spl_w = 0, spl_h = 0;
     uint64_t spl_version = 0;
-    // Lists and camera trees for a new camera are built on a host thread while
-    // frames render without them (same pixels); adopted by the
-    // first frame after the build is done.  (Declared after the structures the
-    // builds read: a pending future's destructor waits for its build.)
+    // Primary sphere lists for a new camera or size are built on a host thread
+    // while frames render without them (same pixels); adopted by the first
+    // frame after the build is done.  (Declared after the structures the
+    // build reads: a pending future's destructor waits for its build.)
     struct SplJob { std::future<PrimarySphereLists> f; CameraModel cam{}; size_t w = 0, h = 0; };
-    struct CamJob {
-        std::future<std::pair<CameraTriangleBVH, PrimaryTriLists>> f;
-        CameraModel cam{}; size_t w = 0, h = 0;
-    };
     SplJob spl_job;
-    CamJob cam_job;
     std::map<int, std::unique_ptr<DeviceState>> devices;
     // one frame at a time per handle: calls from several host threads are
     // serialised here (render_frame_multi re-enters render_frame)
