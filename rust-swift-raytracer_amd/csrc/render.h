@@ -74,6 +74,9 @@ struct TraceParams {
     const uint32_t *sph_kind; // material kind per sphere
     FastDiv div_spp, div_width, div_rowblock;  // job -> (pixel, sample) mapping
     uint32_t refill_min;      // refill dead lanes once at least this many are idle
+    uint32_t walk_min;        // sphere-only: start a walk iteration once this many lanes wait
+                              // for one (0: every iteration walks)
+    uint32_t tri_walk_min;    // triangle scenes: the same for the triangle walk
     uint32_t steps;           // BVH nodes a lane walks per loop iteration (>= 1) ...
     uint32_t step;            // ... when nonzero (else walks run to the end)
     float bvh_c[3], bvh_r, bvh_rmax, bvh_mag, bvh_inv_rmin;

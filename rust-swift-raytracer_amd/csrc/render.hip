@@ -878,7 +878,18 @@ void trace_kernel(TraceParams p) {
             RT_STAMP(1);
             // kStep: at most p.steps node visits per lane per iteration
             uint32_t budget = p.steps;
-            if (kBvh && phase == kSph) {
+            // walk_min (sphere-only scenes): while fewer than walk_min lanes wait
+            // for a walk and other lanes can advance without one (fresh samples
+            // whose primary sphere list replaced the walk), skip this
+            // iteration's walk: those lanes are shaded now and join the next
+            // walk, so fewer walk segments run with lanes idle in them
+            bool walk_now = true;
+            if (!kMesh && p.walk_min != 0) {
+                const uint32_t nwalk = (uint32_t)__popcll(__ballot(phase == kSph));
+                const uint32_t nother = (uint32_t)__popcll(__ballot(phase != kSph && !done));
+                walk_now = nwalk >= p.walk_min || nother == 0;
+            }
+            if (kBvh && phase == kSph && walk_now) {
                 constexpr uint32_t kEnd = kLds ? 0xFFFFu : kNodeEndDev;
                 const SphBound bnd = sph_bound(p, org);
                 F3 nlo, nhi;
@@ -916,7 +927,13 @@ void trace_kernel(TraceParams p) {
                     triangles_brute(p, org, dir, best_t, tri_t, tri_i, tri_in);
                 }
             }
-            if (kMesh && phase == kTri) {
+            bool tri_now = true;
+            if (kMesh && p.tri_walk_min != 0) {
+                const uint32_t nwalk = (uint32_t)__popcll(__ballot(phase == kTri));
+                const uint32_t nother = (uint32_t)__popcll(__ballot(phase != kTri && !done));
+                tri_now = nwalk >= p.tri_walk_min || nother == 0;
+            }
+            if (kMesh && phase == kTri && tri_now) {
                 if (kStep) budget = max(budget, p.steps / 2u);  // a lane that just left the sphere walk
                 const bool cam = bounce == 0 && p.cam_nnodes != 0;
                 const F3 dlt = f3(org.x - p.tbvh_oc[0], org.y - p.tbvh_oc[1], org.z - p.tbvh_oc[2]);
