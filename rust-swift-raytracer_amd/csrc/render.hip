@@ -445,9 +445,9 @@ __device__ __forceinline__ bool tri_begin(const TraceParams &p, F3 org, F3 dir, 
 
 // One node of the triangle tree (static or camera-origin); an entered leaf is
 // handed back in `leaf` as (first << 3) | count, like sphere_node.
-__device__ __forceinline__ bool tri_node(const TraceParams &p, F3 noi, F3 inv, F3 dlt, bool cam,
-                                         float rho, float cap, uint32_t &node,
-                                         uint32_t &leaf, uint32_t &node_tests) {
+__device__ __forceinline__ bool tri_node(const TraceParams &p, F3 nlo, F3 nhi, F3 inv, F3 dlt2, bool cam,
+                                         float cap, uint32_t &node, uint32_t &leaf,
+                                         uint32_t &node_tests) {
     ++node_tests;
     // Quantised nodes (bvh.h QuantGrid): u16 coordinates decoded with one fma
     // on the tree's grid; the host rounds every face outward *after* this
@@ -475,28 +475,30 @@ __device__ __forceinline__ bool tri_node(const TraceParams &p, F3 noi, F3 inv, F
         N1 = make_float4(__builtin_fmaf(hi16(q1.x), ns, nb), __builtin_fmaf(lo16(q1.y), ns, nb),
                          __builtin_fmaf(hi16(q1.y), ns, nb), 0.0f);
     }
-    // s = n^.d over the normal box, d = o - oc (the tree's box origin, bvh.h)
-    const float ax = N0.x * dlt.x, bx = N1.x * dlt.x;
-    const float ay = N0.y * dlt.y, by = N1.y * dlt.y;
-    const float az = N0.z * dlt.z, bz = N1.z * dlt.z;
+    // 2s = n^.(2d) over the normal box, d = o - oc (the tree's box origin,
+    // bvh.h); dlt2 = 2d is exact, so 2s m below has the bits of 2 (s m)
+    const float ax = N0.x * dlt2.x, bx = N1.x * dlt2.x;
+    const float ay = N0.y * dlt2.y, by = N1.y * dlt2.y;
+    const float az = N0.z * dlt2.z, bz = N1.z * dlt2.z;
     const float sl = (fminf(ax, bx) + fminf(ay, by)) + fminf(az, bz);
     const float sh = (fmaxf(ax, bx) + fmaxf(ay, by)) + fmaxf(az, bz);
-    // phantom offset 2 s m_k over s in [sl, sh], m_k in [N0.k, N1.k]
-    auto widen = [&](float lo, float hi, float m0, float m1, float no, float iv, float &t0, float &t1) {
+    // phantom offset 2 s m_k over 2s in [sl, sh], m_k in [N0.k, N1.k]
+    auto widen = [&](float lo, float hi, float m0, float m1, float nl, float nh, float iv, float &t0,
+                     float &t1) {
         const float a = sl * m0, b = sl * m1, c = sh * m0, d = sh * m1;
         const float omin = fminf(fminf(a, b), fminf(c, d));
         const float omax = fmaxf(fmaxf(a, b), fmaxf(c, d));
-        const float l = (lo + 2.0f * omin) - rho;
-        const float h = (hi + 2.0f * omax) + rho;
-        // l * inv - o * inv (noi = -(o * inv)): the face moves by <= u|o| +
-        // 3u|l - o|, far inside rho
-        t0 = __builtin_fmaf(l, iv, no);
-        t1 = __builtin_fmaf(h, iv, no);
+        // (l - (o + rho)) inv and (h - (o - rho)) inv, nl = -((o + rho) inv),
+        // nh = -((o - rho) inv) per ray (sphere_slabs with e = rho): the faces
+        // move out by rho, plus <= u|o + rho| + 3u|l - o| of rounding, far
+        // inside rho
+        t0 = __builtin_fmaf(lo + omin, iv, nl);
+        t1 = __builtin_fmaf(hi + omax, iv, nh);
     };
     float t0x, t1x, t0y, t1y, t0z, t1z;
-    widen(B0.x, B1.x, N0.x, N1.x, noi.x, inv.x, t0x, t1x);
-    widen(B0.y, B1.y, N0.y, N1.y, noi.y, inv.y, t0y, t1y);
-    widen(B0.z, B1.z, N0.z, N1.z, noi.z, inv.z, t0z, t1z);
+    widen(B0.x, B1.x, N0.x, N1.x, nlo.x, nhi.x, inv.x, t0x, t1x);
+    widen(B0.y, B1.y, N0.y, N1.y, nlo.y, nhi.y, inv.y, t0y, t1y);
+    widen(B0.z, B1.z, N0.z, N1.z, nlo.z, nhi.z, inv.z, t0z, t1z);
     const float tn = fmaxf(fmaxf(fminf(t0x, t1x), fminf(t0y, t1y)), fminf(t0z, t1z));
     const float tf = fminf(fminf(fmaxf(t0x, t1x), fmaxf(t0y, t1y)), fmaxf(t0z, t1z));
     // tn > cap as an integer compare (cap > 0 or +inf; see sphere_node: a
@@ -936,12 +938,18 @@ void trace_kernel(TraceParams p) {
             if (kMesh && phase == kTri && tri_now) {
                 if (kStep) budget = max(budget, p.steps / 2u);  // a lane that just left the sphere walk
                 const bool cam = bounce == 0 && p.cam_nnodes != 0;
-                const F3 dlt = f3(org.x - p.tbvh_oc[0], org.y - p.tbvh_oc[1], org.z - p.tbvh_oc[2]);
-                const F3 noi = f3(-(org.x * inv.x), -(org.y * inv.y), -(org.z * inv.z));
+                const F3 dlt2 = f3(2.0f * (org.x - p.tbvh_oc[0]), 2.0f * (org.y - p.tbvh_oc[1]),
+                                   2.0f * (org.z - p.tbvh_oc[2]));
+                // rho (e; 0 on the camera tree) folded into the slab offsets
+                F3 nlo, nhi;
+                sphere_slabs(org, inv, e, nlo, nhi);
+                float cap = fminf(best_t, tri_t);
                 do {
                     uint32_t leaf;
-                    if (tri_node(p, noi, inv, dlt, cam, e, fminf(best_t, tri_t), node, leaf, tnode_tests))
+                    if (tri_node(p, nlo, nhi, inv, dlt2, cam, cap, node, leaf, tnode_tests)) {
                         tri_leaf(p, org, dir, cam, leaf, best_t, tri_t, tri_i, tri_in, tri_done);
+                        cap = fminf(best_t, tri_t);
+                    }
                 } while (node != kNodeEndDev && (!kStep || --budget != 0));
                 if (node == kNodeEndDev) phase = kShade;
             }

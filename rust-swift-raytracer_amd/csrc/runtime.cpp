@@ -494,7 +494,7 @@ int render_frame(WorldState &w, const CameraModel &cam, size_t width, size_t hei
     // 32 -> 6.10); sliced walks refill every iteration (C5: 32 costs +5 %)
     p.refill_min = (uint32_t)std::max<uint64_t>(1, env_u64("RT_AMD_REFILL", p.step ? 1 : 24));
     p.walk_min = (uint32_t)env_u64("RT_AMD_WALK_MIN", 65);  // sphere-only: walk when nothing else can advance
-    p.tri_walk_min = (uint32_t)env_u64("RT_AMD_TRI_WALK_MIN", 0);
+    p.tri_walk_min = (uint32_t)env_u64("RT_AMD_TRI_WALK_MIN", 32);
     const int sv = p.step ? 1 : 0;
     const bool timed = stats != nullptr;  // HIP-event timing + counters need a host wait
     const int ctv = timed ? 1 : 0;         // launch_trace runs the counting variant iff p.stats
