@@ -17,12 +17,14 @@ import sys
 
 
 def short(name):
-    # trace_kernel<kBvh, kLds, kStep, kMesh, kCount>: the timed frames run the
-    # kCount=false variant ("trace_kernel"); frames with stats run
-    # "trace_kernel[count]"
+    # trace_kernel<kBvh, kLds, kStep, kMesh, kCount, kSerial>: the timed frames
+    # run the kCount=false variant ("trace_kernel"); frames with stats run
+    # "trace_kernel[count]", SERIAL passes "trace_kernel[serial]"
     if "trace_kernel" in name:
         args = name.split("trace_kernel<", 1)[-1].split(">", 1)[0].replace(" ", "").split(",")
-        return "trace_kernel[count]" if len(args) == 5 and args[4] == "true" else "trace_kernel"
+        if len(args) >= 6 and args[5] == "true":
+            return "trace_kernel[serial]"
+        return "trace_kernel[count]" if len(args) >= 5 and args[4] == "true" else "trace_kernel"
     if "resolve_kernel" in name:
         return "resolve_kernel"
     return name[:60]
