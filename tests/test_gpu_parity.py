@@ -256,8 +256,9 @@ def test_slabs_do_not_change_the_frame(monkeypatch):
 
 @pytest.mark.parametrize("scene", ["rtow", "mesh_soup"])
 def test_scheduling_knobs_do_not_change_samples(monkeypatch, scene):
-    """Job-queue partitions, chunk size, walk slicing, the tree's memory (LDS
-    or global) and the inflation bound only change work, never a sample."""
+    """Job-queue partitions, chunk size, walk slicing and gating, the tree's
+    memory (LDS or global) and the inflation bound only change work, never a
+    sample."""
     src = scene_text("rtow.txt") if scene == "rtow" else _triangle_scene(41, 400, spheres=40)
     w, h, spp = 160, 90, 4
     world = R.World(src)
@@ -270,7 +271,11 @@ def test_scheduling_knobs_do_not_change_samples(monkeypatch, scene):
                 dict(RT_AMD_LDS="0", RT_AMD_STEP="1", RT_AMD_STEPS="3"),
                 dict(RT_AMD_LINEAR_E="1"), dict(RT_AMD_PRIMARY_LISTS="0"),
                 dict(RT_AMD_SPHERE_LISTS="0"), dict(RT_AMD_FUSED="0"),
-                dict(RT_AMD_RESOLVE_PIX="1"), dict(RT_AMD_RESOLVE_PIX="64")]:
+                dict(RT_AMD_RESOLVE_PIX="1"), dict(RT_AMD_RESOLVE_PIX="64"),
+                # walk gating: every iteration walks / walks once 8 lanes wait
+                dict(RT_AMD_WALK_MIN="0"), dict(RT_AMD_WALK_MIN="8", RT_AMD_REFILL="5"),
+                dict(RT_AMD_TRI_WALK_MIN="0"), dict(RT_AMD_TRI_WALK_MIN="65"),
+                dict(RT_AMD_STEP="1", RT_AMD_STEPS="7", RT_AMD_WALK_MIN="65")]:
         for k, v in env.items():
             monkeypatch.setenv(k, v)
         out, _ = render_kept(world, w, h, spp, 8)
