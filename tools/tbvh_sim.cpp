@@ -6,6 +6,13 @@
 // builder layout, whose sibling pairs and top levels sit together.)
 // Not product code and not a parity check: float arithmetic mirrors the
 // kernel's box test; hits use the reference's triangle t (with its sign).
+// Experiments:
+//   SIM_OC=x,y,z[,L]  static tree built for origin (x,y,z) [SAH phantom scale L]
+//   SIM_CELL=S        one tree per S-unit cell of the secondary-ray origins
+//   SIM_HYB=D,S       the static topology with per-cell boxes (phantoms at the
+//                     cell centre, widened per ray from it) for depth < D
+//   SIM_HYB_RANGE=1   ... boxes over the whole cell instead (no widening)
+//   SIM_LEVELS=1      share of visits per tree level
 //   g++ -O2 -std=c++17 -I../rust-swift-raytracer_amd/csrc tbvh_sim.cpp \
 //       ../rust-swift-raytracer_amd/csrc/{bvh,scene}.cpp -o tbvh_sim
 #include <cmath>
@@ -13,6 +20,8 @@
 #include <cstdlib>
 #include <fstream>
 #include <map>
+#include <functional>
+#include <algorithm>
 #include <tuple>
 #include <vector>
 #include <sstream>
@@ -34,7 +43,12 @@ struct Count { double nodes = 0, tests = 0, rays = 0; };
 static std::vector<int> g_depth;          // node depth (kernel image), for SIM_LEVELS
 static std::vector<double> g_level_visits;
 
-static bool g_exact = false;  // tree over phantom triangles of one origin (no widening)
+static bool g_exact = false;
+static int g_hyb_D = 0;                       // SIM_HYB=D,S: per-cell boxes for depth < D
+static const std::vector<float> *g_cellbox = nullptr;  // 6 per node (lo, hi) for this ray's cell
+static double g_hyb_hits = 0;
+static float g_coc[3];
+static bool g_hyb_range = false;  // SIM_HYB_RANGE=1: boxes over the whole cell, no widening  // tree over phantom triangles of one origin (no widening)
 
 // Walks the kernel image (bvh.h qnodes: builder layout, fixed child-a-first
 // order, one link per node) with the kernel's box arithmetic.
@@ -64,6 +78,23 @@ static float trace(const TriangleBVH &t, V o, V d, Count &c) {
             sl += std::fmin(a, b); sh += std::fmax(a, b);
         }
         float tn = -INFINITY, tf = INFINITY;
+        if (g_cellbox && g_depth[node] < g_hyb_D) {
+            g_hyb_hits += 1;
+            const float *cb = &(*g_cellbox)[(size_t)node * 6];
+            float csl = 0, csh = 0;
+            for (int k = 0; k < 3 && !g_hyb_range; ++k) {
+                float a = n0[k] * (ov[k] - g_coc[k]), b = n1[k] * (ov[k] - g_coc[k]);
+                csl += std::fmin(a, b); csh += std::fmax(a, b);
+            }
+            for (int k = 0; k < 3; ++k) {
+                float a = csl * n0[k], b = csl * n1[k], cc = csh * n0[k], dd = csh * n1[k];
+                float lo = cb[k] + 2 * std::fmin(std::fmin(a, b), std::fmin(cc, dd)) - rho;
+                float hi = cb[3 + k] + 2 * std::fmax(std::fmax(a, b), std::fmax(cc, dd)) + rho;
+                float t0 = (lo - ov[k]) * iv[k], t1 = (hi - ov[k]) * iv[k];
+                tn = std::fmax(tn, std::fmin(t0, t1));
+                tf = std::fmin(tf, std::fmax(t0, t1));
+            }
+        } else
         for (int k = 0; k < 3; ++k) {
             float a = sl * n0[k], b = sl * n1[k], cc = sh * n0[k], dd = sh * n1[k];
             float lo = dec(u[k], t.qbox.step[k], t.qbox.base[k]) + 2 * std::fmin(std::fmin(a, b), std::fmin(cc, dd)) - rho;
@@ -109,7 +140,11 @@ int main(int argc, char **argv) {
     const int W = argc > 3 ? std::atoi(argv[2]) : 96, H = argc > 3 ? std::atoi(argv[3]) : 54;
     PackedScene p = pack_scene(s, 8, 1);
     const char *lf = std::getenv("RT_AMD_TRI_LEAF");
-    TriangleBVH t = build_triangle_bvh(s.triangles, p.tri_hot, lf ? std::atoi(lf) : 4);
+    float soc[3] = {0, 0, 0};
+    const char *socs = std::getenv("SIM_OC");  // static-tree origin "x,y,z" (+ optional ",L")
+    double sph = 0;
+    if (socs) std::sscanf(socs, "%f,%f,%f,%lf", &soc[0], &soc[1], &soc[2], &sph);
+    TriangleBVH t = build_triangle_bvh(s.triangles, p.tri_hot, lf ? std::atoi(lf) : 4, socs ? soc : nullptr, sph);
     std::printf("tris %zu nodes %zu loose %zu depth %u\n", s.triangles.size(), t.nodes.size() / 16,
                 t.loose.size(), t.depth);
     if (std::getenv("SIM_LEVELS")) {  // depth of every node (child pair at a & 0x1FFFFFFF)
@@ -161,6 +196,92 @@ int main(int argc, char **argv) {
                 trace(t, o2, d2, sec);
             }
         }
+    if (const char *hs = std::getenv("SIM_HYB")) {
+        float S = 1; std::sscanf(hs, "%d,%f", &g_hyb_D, &S);
+        g_hyb_range = std::getenv("SIM_HYB_RANGE") != nullptr;
+        const size_t n = t.qnodes.size() / 8;
+        g_depth.assign(n, 0);
+        g_level_visits.assign(64, 0);
+        for (size_t i = 0; i < n; ++i) {
+            const uint32_t a = t.qnodes[i * 8 + 6];
+            if (!(a & kLeafBit)) { const uint32_t ch = a & 0x1FFFFFFFu; g_depth[ch] = g_depth[ch + 1] = g_depth[i] + 1; }
+        }
+        std::vector<V> o2s, d2s;
+        uint32_t rng2 = 2547549u;
+        auto rnd2 = [&]() { rng2 ^= rng2 << 13; rng2 ^= rng2 >> 17; rng2 ^= rng2 << 5; return rng2 * 0x1p-32f; };
+        Count dummy;
+        for (int j = 0; j < H; ++j)
+            for (int i = 0; i < W; ++i) {
+                float u = (i + 0.5f) / W, v = (j + 0.5f) / H;
+                V d = unit(sub(add(add(V{cm.lower_left.x, cm.lower_left.y, cm.lower_left.z},
+                                       mul(V{cm.horizontal.x, cm.horizontal.y, cm.horizontal.z}, u)),
+                                   mul(V{cm.vertical.x, cm.vertical.y, cm.vertical.z}, v)), org));
+                float tt = trace(t, org, d, dummy);
+                if (std::isfinite(tt)) {
+                    o2s.push_back(add(org, mul(d, tt)));
+                    d2s.push_back(unit(V{rnd2() * 2 - 1, rnd2() * 2 - 1, rnd2() * 2 - 1}));
+                }
+            }
+        std::map<std::tuple<int, int, int>, std::vector<float>> cells;
+        // per-node box over the node's records' phantoms for o in the cell
+        std::function<void(uint32_t, const double *, const double *, std::vector<float> &, float *)> rec;
+        rec = [&](uint32_t node, const double *clo, const double *chi, std::vector<float> &out, float *bx) {
+            const uint32_t a = t.qnodes[(size_t)node * 8 + 6];
+            float b[6] = {INFINITY, INFINITY, INFINITY, -INFINITY, -INFINITY, -INFINITY};
+            if (a & kLeafBit) {
+                const uint32_t first = (a & ~kLeafBit) >> 3, count = a & 7u;
+                for (uint32_t j = first; j < first + count; ++j) {
+                    const float *r = &t.tris[(size_t)j * 16];
+                    double nn = std::sqrt((double)r[0] * r[0] + (double)r[1] * r[1] + (double)r[2] * r[2]);
+                    double nh[3] = {r[0] / nn, r[1] / nn, r[2] / nn};
+                    double smin = 0, smax = 0;
+                    for (int k = 0; k < 3; ++k) {
+                        if (g_hyb_range) {
+                            const double p = nh[k] * clo[k], q = nh[k] * chi[k];
+                            smin += std::min(p, q);
+                            smax += std::max(p, q);
+                        } else {
+                            smin += nh[k] * (clo[k] + chi[k]) / 2;
+                        }
+                    }
+                    if (!g_hyb_range) smax = smin;
+                    for (int k = 0; k < 3; ++k) {
+                        double o1 = 2 * nh[k] * smin, o2 = 2 * nh[k] * smax;
+                        double vmin = std::min({r[4 + k], r[8 + k], r[12 + k]}), vmax = std::max({r[4 + k], r[8 + k], r[12 + k]});
+                        b[k] = std::min(b[k], (float)(vmin + std::min(o1, o2)) - 1e-4f);
+                        b[3 + k] = std::max(b[3 + k], (float)(vmax + std::max(o1, o2)) + 1e-4f);
+                    }
+                }
+            } else {
+                const uint32_t ch = a & 0x1FFFFFFFu;
+                float b1[6], b2[6];
+                rec(ch, clo, chi, out, b1); rec(ch + 1, clo, chi, out, b2);
+                for (int k = 0; k < 3; ++k) { b[k] = std::min(b1[k], b2[k]); b[3 + k] = std::max(b1[3 + k], b2[3 + k]); }
+            }
+            for (int k = 0; k < 6; ++k) { bx[k] = b[k]; out[(size_t)node * 6 + k] = b[k]; }
+        };
+        Count hc;
+        for (size_t r = 0; r < o2s.size(); ++r) {
+            V o2 = o2s[r];
+            auto key = std::make_tuple((int)std::floor(o2.x / S), (int)std::floor(o2.y / S), (int)std::floor(o2.z / S));
+            auto it = cells.find(key);
+            if (it == cells.end()) {
+                double clo[3] = {std::get<0>(key) * S, std::get<1>(key) * S, std::get<2>(key) * S};
+                double chi[3] = {clo[0] + S, clo[1] + S, clo[2] + S};
+                std::vector<float> bx(n * 6);
+                float root[6];
+                rec(0, clo, chi, bx, root);
+                it = cells.emplace(key, std::move(bx)).first;
+            }
+            g_cellbox = &it->second;
+            for (int k = 0; k < 3; ++k) g_coc[k] = (k == 0 ? std::get<0>(key) : k == 1 ? std::get<1>(key) : std::get<2>(key)) * S + S / 2;
+            trace(t, o2, d2s[r], hc);
+            g_cellbox = nullptr;
+        }
+        std::printf("hybrid D=%d S=%g: %zu cells, secondary %.1f nodes/ray (%.1f with cell boxes), %.2f tests/ray\n",
+                    g_hyb_D, S, cells.size(), hc.nodes / hc.rays, g_hyb_hits / hc.rays, hc.tests / hc.rays);
+        return 0;
+    }
     if (const char *cs = std::getenv("SIM_CELL")) {  // per-cell trees for the secondary rays
         const float S = std::atof(cs);
         // secondary origins: the primary hit points (recomputed)
