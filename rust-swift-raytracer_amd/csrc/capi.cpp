@@ -59,9 +59,11 @@ Rust_WorldHandle *load_world(const char *source) {
     }
     // spheres padded to the kernel's scalar-load batch of 8 with NaN centres
     world->state.packed = rtamd::pack_scene(world->state.scene, 8, 1);
-    const char *leaf = std::getenv("RT_AMD_LEAF");  // tuning knob: spheres per BVH leaf
+    // spheres per BVH leaf (A/B with walk gating, C2 / C3: 3 -> 4.72 / 70.6 ms,
+    // 2 -> 4.65 / 69.6, 1 -> 6.33 / 95.3 -- its tree no longer fits 64 KB of LDS)
+    const char *leaf = std::getenv("RT_AMD_LEAF");
     world->state.bvh = rtamd::build_sphere_bvh(world->state.scene.spheres,
-                                               leaf ? (uint32_t)std::atoi(leaf) : 3u);
+                                               leaf ? (uint32_t)std::atoi(leaf) : 2u);
     // triangles per BVH leaf (A/B on C5 at 96-node walk slices: 1 -> 222 ms,
     // 2 -> 240, 3 -> 293)
     const char *tleaf = std::getenv("RT_AMD_TRI_LEAF");

@@ -294,7 +294,7 @@ def test_tree_shape_knobs_do_not_change_samples(monkeypatch, scene):
     src = scene_text("rtow.txt") if scene == "rtow" else _triangle_scene(41, 400, spheres=40)
     w, h, spp = 96, 54, 4
     ref, _ = render_kept(R.World(src), w, h, spp, 8)
-    for env in [dict(RT_AMD_LEAF="1"), dict(RT_AMD_LEAF="7"), dict(RT_AMD_TRI_LEAF="2"),
+    for env in [dict(RT_AMD_LEAF="1"), dict(RT_AMD_LEAF="3"), dict(RT_AMD_LEAF="7"), dict(RT_AMD_TRI_LEAF="2"),
                 dict(RT_AMD_TRI_LEAF="7"), dict(RT_AMD_CAM_LEAF="1"), dict(RT_AMD_CAM_LEAF="5"),
                 dict(RT_AMD_TRI_PHANTOM="0.5"), dict(RT_AMD_BIG_K="2"),
                 dict(RT_AMD_BIG_K="1e9"), dict(RT_AMD_BIG_K="0")]:
