@@ -467,14 +467,16 @@ __device__ __forceinline__ bool tri_node(const TraceParams &p, F3 nlo, F3 nhi, F
                                   __builtin_fmaf(lo16(q0.y), gsz, gbz), 0.0f);
     const float4 B1 = make_float4(__builtin_fmaf(hi16(q0.y), gsx, gbx), __builtin_fmaf(lo16(q0.z), gsy, gby),
                                   __builtin_fmaf(hi16(q0.z), gsz, gbz), 0.0f);
-    float4 N0 = make_float4(0.0f, 0.0f, 0.0f, 0.0f), N1 = N0;  // camera tree: no widening
-    if (!cam) {
-        const float nb = p.tq_nbase, ns = p.tq_nstep;
-        N0 = make_float4(__builtin_fmaf(lo16(q0.w), ns, nb), __builtin_fmaf(hi16(q0.w), ns, nb),
-                         __builtin_fmaf(lo16(q1.x), ns, nb), 0.0f);
-        N1 = make_float4(__builtin_fmaf(hi16(q1.x), ns, nb), __builtin_fmaf(lo16(q1.y), ns, nb),
-                         __builtin_fmaf(hi16(q1.y), ns, nb), 0.0f);
-    }
+    // normal box; the camera tree has none (no widening): its lanes decode
+    // with a zero grid, so every word of the node is used on every path and
+    // the node stays two 16-B loads (with the decode under `if (!cam)` the
+    // compiler split the second half into a dword and a dwordx3 load: three
+    // memory instructions per node, C5 +24 %)
+    const float nb = cam ? 0.0f : p.tq_nbase, ns = cam ? 0.0f : p.tq_nstep;
+    const float4 N0 = make_float4(__builtin_fmaf(lo16(q0.w), ns, nb), __builtin_fmaf(hi16(q0.w), ns, nb),
+                                  __builtin_fmaf(lo16(q1.x), ns, nb), 0.0f);
+    const float4 N1 = make_float4(__builtin_fmaf(hi16(q1.x), ns, nb), __builtin_fmaf(lo16(q1.y), ns, nb),
+                                  __builtin_fmaf(hi16(q1.y), ns, nb), 0.0f);
     // 2s = n^.(2d) over the normal box, d = o - oc (the tree's box origin,
     // bvh.h); dlt2 = 2d is exact, so 2s m below has the bits of 2 (s m)
     const float ax = N0.x * dlt2.x, bx = N1.x * dlt2.x;
