@@ -377,7 +377,7 @@ int render_frame(WorldState &w, const CameraModel &cam, size_t width, size_t hei
     // node visits per lane per loop iteration of a sliced walk (A/B on C5, 8
     // waves per SIMD: 32 -> 277 ms, 64 -> 259, 96 -> 252, 128 -> 248, 192 ->
     // 251, 256 -> 263, 512 -> 353; 6 waves: 64 -> 243, 96 -> 240, 128 -> 242)
-    p.steps = (uint32_t)std::max<uint64_t>(1, env_u64("RT_AMD_STEPS", 96));
+    p.steps = (uint32_t)std::max<uint64_t>(1, env_u64("RT_AMD_STEPS", 128));
     p.row_block = B; p.rank = o.rank; p.nranks = nranks;
     const bool use_bvh = d->nnodes > 0 && o.accel != RT_ACCEL_BRUTE;
     if (use_bvh) {
