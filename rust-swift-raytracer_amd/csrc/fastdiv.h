@@ -18,7 +18,7 @@ namespace rtamd {
 struct FastDiv {
     uint32_t m, s, one, d;
 };
-inline FastDiv make_fastdiv(uint32_t d) {
+RT_HOST_DEVICE inline FastDiv make_fastdiv(uint32_t d) {
     FastDiv f{0, 0, d <= 1u ? 1u : 0u, d ? d : 1u};
     if (d > 1) {
         uint32_t l = 0;

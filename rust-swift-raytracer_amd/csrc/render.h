@@ -134,9 +134,9 @@ RT_HOST_DEVICE inline uint32_t serial_lo(const double *M, uint32_t a, uint32_t j
 
 hipError_t launch_trace(const TraceParams &p, uint32_t blocks, hipStream_t stream);
 // SERIAL mode.  ctrl (u32[8]): {resolved, state at sample a, sum of b (low
-// bits), iterations, a = first unresolved sample, 0, iterations that stopped
-// short, 0}.  jump: 64 x 32 u32, column c of M^(2^i) (xorshift32 is linear
-// over GF(2)).  Window: win[i] = xorshift32^i(ctrl[1]) for i < n.
+// bits), iterations, a = first unresolved sample, candidates per sample of the
+// next iteration (0: the launch's K), iterations that stopped short, 0}.
+// jump: 64 x 32 u32, column c of M^(2^i) (xorshift32 is linear over GF(2)).  Window: win[i] = xorshift32^i(ctrl[1]) for i < n.
 hipError_t launch_serial_window(const uint32_t *ctrl, const uint32_t *jump, uint32_t *win, uint32_t n,
                                 hipStream_t stream);
 // Walk: from sample a = ctrl[4], follows the true path through the candidate
@@ -146,7 +146,13 @@ hipError_t launch_serial_window(const uint32_t *ctrl, const uint32_t *jump, uint
 // ctrl (a, the state at a, resolved).  bend: scratch of
 // ceil(L / serial_walk_block(L)) * K u32.
 uint32_t serial_walk_block(uint32_t L);
-hipError_t launch_serial_walk(uint32_t *ctrl, const float *table, const double *M, const uint32_t *win,
+// V (optional): the per-sample scatter-count variances as npix + 1 per-pixel
+// prefix sums of spp var followed by npix per-pixel variances; with it
+// the walk sets the next iteration's candidates per sample in ctrl[5] (<= K):
+// 2 z (sqrt(V over its L samples) + sfloor sqrt(L)) + 2 depth + 2; the count
+// pass and the walks use ctrl[5] when it is set.
+hipError_t launch_serial_walk(uint32_t *ctrl, const float *table, const double *M, const double *V,
+                              uint32_t npix, uint32_t spp, float z, float sfloor, const uint32_t *win,
                               uint32_t *states, uint32_t *bend, uint32_t L, uint32_t K, uint32_t depth,
                               uint32_t nserial, hipStream_t stream);
 // inv_spp = 1.0 / (spp as f32) computed from the signed spp (common.rs:345).

@@ -698,9 +698,17 @@ __global__ __launch_bounds__(kLds ? (kMesh ? RT_LDS_BLOCK_MESH : RT_LDS_BLOCK_SP
 __attribute__((amdgpu_waves_per_eu((kMesh && !kCount) ? RT_WAVES_PER_EU_MESH : RT_WAVES_PER_EU, 8)))
 void trace_kernel(TraceParams p) {
     // SERIAL count passes: the walk of the previous pass set the first sample
+    // and this iteration's candidates per sample (ctrl[5], <= the launch's K)
     if (kSerial && p.ctrl != nullptr) {
         if (p.ctrl[0] != 0u) return;
         p.cbase = p.ctrl[4];  // (the walks advance it)
+        const uint32_t K = p.ctrl[5];
+        if (p.mode == kRngSerialCount && K != 0u && K < p.spp) {
+            p.chunk = (p.chunk / K) * K;  // (whole samples, about as many jobs per atomic)
+            p.spp = K;
+            p.div_spp = make_fastdiv(K);
+            p.njobs = p.npix * K;
+        }
     }
     const uint32_t lane = __lane_id();
     extern __shared__ float4 lds[];
@@ -1418,10 +1426,17 @@ __device__ __forceinline__ uint32_t walk_step(const float *table, const double *
     return b >= 0.0f ? B + (uint32_t)b : kWalkInvalid;
 }
 
+// (the iteration's candidates per sample: ctrl[5] when set, else the launch's K)
+__device__ __forceinline__ uint32_t serial_k(const uint32_t *ctrl, uint32_t K) {
+    const uint32_t k = ctrl[5];
+    return k != 0u && k < K ? k : K;
+}
+
 __global__ __launch_bounds__(256) void serial_walk_blocks_kernel(
     const uint32_t *__restrict__ ctrl, const float *__restrict__ table, const double *__restrict__ M,
     uint32_t *__restrict__ bend, uint32_t L, uint32_t K, uint32_t R, uint32_t depth, uint32_t nserial) {
     if (ctrl[0] != 0u) return;
+    K = serial_k(ctrl, K);
     const uint32_t a = ctrl[4];
     const uint32_t n = min(L, nserial - a);
     const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1437,11 +1452,13 @@ __global__ __launch_bounds__(256) void serial_walk_blocks_kernel(
 
 __global__ __launch_bounds__(256) void serial_walk_finish_kernel(
     uint32_t *__restrict__ ctrl, const float *__restrict__ table, const double *__restrict__ M,
-    const uint32_t *__restrict__ win, const uint32_t *__restrict__ bend, uint32_t *__restrict__ states,
-    uint32_t L, uint32_t K, uint32_t R, uint32_t depth, uint32_t nserial) {
+    const double *__restrict__ V, uint32_t npix, uint32_t spp, const uint32_t *__restrict__ win,
+    const uint32_t *__restrict__ bend, uint32_t *__restrict__ states, uint32_t L, uint32_t Kmax, uint32_t R,
+    uint32_t depth, uint32_t nserial, float z, float sfloor) {
     __shared__ uint32_t bstart[256];
     __shared__ uint32_t nfull;
     if (ctrl[0] != 0u) return;
+    const uint32_t K = serial_k(ctrl, Kmax);
     const uint32_t a = ctrl[4];
     const uint32_t n = min(L, nserial - a);
     const uint32_t nb = (n + R - 1) / R;
@@ -1475,6 +1492,23 @@ __global__ __launch_bounds__(256) void serial_walk_finish_kernel(
         ctrl[3] += 1u;
         ctrl[4] = a + done;
         if (a + done >= nserial) ctrl[0] = 1u;
+        if (V != nullptr) {
+            // the next iteration's windows: +-z sigma of the scatter-count
+            // deviation its samples can accumulate (V: prefix sums of the
+            // per-sample variances from the estimate pass), plus the spread of
+            // one sample; never more than the launch's Kmax
+            // V: per-pixel prefix sums P (npix + 1) then variances (npix); the
+            // variance of samples [0, j) is P[p] + (j - p spp) var[p], p = j / spp
+            auto vsum = [&](uint32_t j) {
+                const uint32_t q = min(j / spp, npix);
+                return q < npix ? V[q] + (double)(j - q * spp) * V[npix + 1 + q] : V[npix];
+            };
+            const uint32_t a2 = min(a + done, nserial), e = min(a2 + L, nserial);
+            const double v = vsum(e) - vsum(a2);
+            const double w = ceil(2.0 * (double)z * (sqrt(v > 0.0 ? v : 0.0) + (double)sfloor * sqrt((double)(e - a2)))) +
+                             (double)(2u * depth + 2u);
+            ctrl[5] = w >= (double)Kmax ? Kmax : (uint32_t)w;
+        }
     }
     __syncthreads();
     for (uint32_t blk = threadIdx.x; blk < nfull; blk += blockDim.x) {
@@ -1501,7 +1535,8 @@ uint32_t serial_walk_block(uint32_t L) {
     return R < 32u ? 32u : R;
 }
 
-hipError_t launch_serial_walk(uint32_t *ctrl, const float *table, const double *M, const uint32_t *win,
+hipError_t launch_serial_walk(uint32_t *ctrl, const float *table, const double *M, const double *V,
+                              uint32_t npix, uint32_t spp, float z, float sfloor, const uint32_t *win,
                               uint32_t *states, uint32_t *bend, uint32_t L, uint32_t K, uint32_t depth,
                               uint32_t nserial, hipStream_t stream) {
     if (!L) return hipSuccess;
@@ -1509,8 +1544,8 @@ hipError_t launch_serial_walk(uint32_t *ctrl, const float *table, const double *
     const uint64_t nt = (uint64_t)((L + R - 1) / R) * K;
     hipLaunchKernelGGL(serial_walk_blocks_kernel, dim3((uint32_t)((nt + 255) / 256)), dim3(256), 0, stream,
                        ctrl, table, M, bend, L, K, R, depth, nserial);
-    hipLaunchKernelGGL(serial_walk_finish_kernel, dim3(1), dim3(256), 0, stream, ctrl, table, M, win, bend,
-                       states, L, K, R, depth, nserial);
+    hipLaunchKernelGGL(serial_walk_finish_kernel, dim3(1), dim3(256), 0, stream, ctrl, table, M, V, npix,
+                       spp ? spp : 1u, win, bend, states, L, K, R, depth, nserial, z, sfloor);
     return hipGetLastError();
 }
 

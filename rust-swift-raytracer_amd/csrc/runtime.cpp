@@ -53,7 +53,7 @@ DeviceState::~DeviceState() {
                     bvh_nodes, bvh_prims, big_hot, bvh_miss, bvh_prim_id, big_id, bvh_miss16,
                     sph_shade, sph_kind, tbvh_nodes, tbvh_tris, tbvh_loose,
                     cam_nodes, cam_tris, ptl_off, ptl_items, spl, tile, gath,
-                    sstates, sM, swin, sjump, sctrl, sbend};
+                    sstates, sM, sV, swin, sjump, sctrl, sbend};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
     for (hipEvent_t e : ev)
@@ -701,6 +701,10 @@ std::vector<uint32_t> xorshift_jump_table() {
 }
 }  // namespace
 
+// sigma floor of a sample's scatter count (the frame-wide K adds 0.05 to its
+// sigma), scaled for the means' estimation error from `per` traces a pixel
+static double serial_floor(uint64_t per) { return 0.05 * std::sqrt(1.0 + 1.0 / (double)per); }
+
 int render_frame_serial(WorldState &w, const CameraModel &cam, size_t width, size_t height,
                         const RtRenderOptions &o, uint32_t *d_out, hipStream_t stream,
                         RtRenderStats *stats) {
@@ -731,15 +735,15 @@ int render_frame_serial(WorldState &w, const CameraModel &cam, size_t width, siz
     ob.nranks = 1;
     ob.flags = 0;
     if (N > 0) {
+        const auto tp0 = std::chrono::steady_clock::now();  // (RT_AMD_SERIAL_DEBUG)
         // 1. per-pixel mean scatter counts from R counter-seeded traces per sample
         const uint64_t R = std::max<uint64_t>(
             1, std::min<uint64_t>({(32 + spp - 1) / spp, 16, 0x7FFFFFFFull / N}));
         const uint64_t npix = (uint64_t)width * height;
-        std::vector<double> mu(npix, 0.0);
+        std::vector<double> mu(npix, 0.0), sq(npix, 0.0);
         double ss = 0.0;  // within-pixel sum of squares (sigma of one sample's b)
         {
             std::vector<float> est;
-            std::vector<double> sq(npix, 0.0);
             const uint64_t step = std::max<uint64_t>(1, (1ull << 28) / R);
             for (uint64_t c0 = 0; c0 < N; c0 += step) {
                 const uint32_t n = (uint32_t)std::min<uint64_t>(step, N - c0);
@@ -793,6 +797,29 @@ int render_frame_serial(WorldState &w, const CameraModel &cam, size_t width, siz
         std::vector<double> M(N + 1);
         M[0] = 0.0;
         for (uint64_t j = 0; j < N; ++j) M[j + 1] = M[j] + mu[j / spp];
+        // and of each sample's variance around it (the pixel's own, scaled for the
+        // means' estimation error): the walks size each iteration's windows
+        // from it, 2 z (sqrt(V) + 0.05 sqrt(n scale)) + 2 depth + 2 for n
+        // samples -- the frame-wide K above where every pixel has the frame's
+        // sigma, narrower over sky and other constant-count pixels
+        // (per pixel: V(j) = P[p] + (j - p spp) var[p] for sample j of pixel p,
+        // with P the prefix sums over pixels of spp var: npix + 1 and npix
+        // doubles instead of N + 1)
+        const bool adapt = env_u64("RT_AMD_SERIAL_ADAPT", 1) != 0;
+        std::vector<double> V;  // [P (npix + 1) | var (npix)]
+        if (adapt) {
+            V.assign(2 * npix + 1, 0.0);
+            const double per = (double)(spp * R), scale = 1.0 + 1.0 / per;
+            for (uint64_t q = 0; q < npix; ++q) {
+                const double v = std::max(sq[q] / per - mu[q] * mu[q], 0.0) * scale;
+                V[npix + 1 + q] = v;
+                V[q + 1] = V[q] + (double)spp * v;
+            }
+        }
+        auto vsum = [&](uint64_t j) {  // V(j): variance of samples [0, j)
+            const uint64_t q = std::min<uint64_t>(j / spp, npix);
+            return q < npix ? V[q] + (double)(j - q * spp) * V[npix + 1 + q] : V[npix];
+        };
         double dmax = 0.0;  // largest predicted offset within L samples: the window
         for (uint64_t a = 0; a < N; a += std::max<uint64_t>(1, L / 4))
             dmax = std::max(dmax, M[std::min(N, a + L + L / 4)] - M[a]);
@@ -804,6 +831,14 @@ int render_frame_serial(WorldState &w, const CameraModel &cam, size_t width, siz
         const uint64_t R_walk = serial_walk_block((uint32_t)L);
         HIP_TRY(grow(d->sM, d->sM_cap, N + 1));
         HIP_TRY(hipMemcpyAsync(d->sM, M.data(), (N + 1) * 8, hipMemcpyHostToDevice, s));
+        uint32_t K0 = 0;  // the first iteration's candidates (later ones: the walks)
+        if (adapt) {
+            HIP_TRY(grow(d->sV, d->sV_cap, V.size()));
+            HIP_TRY(hipMemcpyAsync(d->sV, V.data(), V.size() * 8, hipMemcpyHostToDevice, s));
+            const uint64_t n0 = std::min(N, L);
+            const double w0 = 2.0 * z * (std::sqrt(vsum(n0)) + serial_floor(spp * R) * std::sqrt((double)n0));
+            K0 = (uint32_t)std::min<double>((double)K, std::ceil(w0) + 2.0 * depth + 2.0);
+        }
         HIP_TRY(grow(d->swin, d->swin_cap, wlen));
         HIP_TRY(grow(d->sbend, d->sbend_cap, (L + R_walk - 1) / R_walk * K));
         if (!d->sjump) {
@@ -812,12 +847,18 @@ int render_frame_serial(WorldState &w, const CameraModel &cam, size_t width, siz
             HIP_TRY(hipMemcpy(d->sjump, jt.data(), jt.size() * 4, hipMemcpyHostToDevice));
         }
         if (!d->sctrl) HIP_TRY(hipMalloc((void **)&d->sctrl, 32));
-        const uint32_t ctrl0[8] = {0u, o.seed, 0u, 0u, 0u, 0u, 0u, 0u};  // Random::new() (random.rs:8-10)
+        const uint32_t ctrl0[8] = {0u, o.seed, 0u, 0u, 0u, K0, 0u, 0u};  // Random::new() (random.rs:8-10)
         HIP_TRY(hipMemcpyAsync(d->sctrl, ctrl0, 32, hipMemcpyHostToDevice, s));
         // iterations are queued in batches sized by the expected progress;
         // those queued past the end exit at once (ctrl[0])
         uint32_t ctrl[8] = {0, 0, 0, 0, 0, 0, 0, 0};
         double t_enqueue = 0, t_wait = 0;  // (RT_AMD_SERIAL_DEBUG)
+        hipEvent_t dbg_ev[2] = {nullptr, nullptr};
+        if (env_u64("RT_AMD_SERIAL_DEBUG", 0)) {
+            for (auto &e : dbg_ev) HIP_TRY(hipEventCreate(&e));
+            HIP_TRY(hipEventRecord(dbg_ev[0], s));
+        }
+        const double t_prep = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tp0).count();
         uint64_t queued = 0;
         while (!ctrl[0]) {
             const uint64_t left = N - ctrl[4];
@@ -833,8 +874,10 @@ int render_frame_serial(WorldState &w, const CameraModel &cam, size_t width, siz
                                     d->sctrl};
                 rc = render_frame(w, cam, width, height, ob, nullptr, s, nullptr, &sp);
                 if (rc) return rc;
-                HIP_TRY(launch_serial_walk(d->sctrl, d->samples, d->sM, d->swin, d->sstates, d->sbend,
-                                           (uint32_t)L, (uint32_t)K, depth, (uint32_t)N, s));
+                HIP_TRY(launch_serial_walk(d->sctrl, d->samples, d->sM, adapt ? d->sV : nullptr,
+                                           (uint32_t)npix, (uint32_t)spp, (float)z, (float)serial_floor(spp * R),
+                                           d->swin, d->sstates, d->sbend, (uint32_t)L, (uint32_t)K, depth,
+                                           (uint32_t)N, s));
             }
             const auto t1 = std::chrono::steady_clock::now();
             HIP_TRY(hipMemcpyAsync(ctrl, d->sctrl, 32, hipMemcpyDeviceToHost, s));
@@ -844,11 +887,20 @@ int render_frame_serial(WorldState &w, const CameraModel &cam, size_t width, siz
             t_wait += std::chrono::duration<double, std::milli>(t2 - t1).count();
         }
         if (stats) stats->serial_retries = ctrl[6];
+        if (dbg_ev[0]) {
+            HIP_TRY(hipEventRecord(dbg_ev[1], s));
+            HIP_TRY(hipEventSynchronize(dbg_ev[1]));
+            float a = 0, b = 0;
+            HIP_TRY(hipEventElapsedTime(&a, d->sev[0], dbg_ev[0]));
+            HIP_TRY(hipEventElapsedTime(&b, dbg_ev[0], dbg_ev[1]));
+            std::fprintf(stderr, "serial debug: GPU estimate + tables %.1f ms, iterations %.1f ms\n", a, b);
+            for (auto &e : dbg_ev) (void)hipEventDestroy(e);
+        }
         if (env_u64("RT_AMD_SERIAL_DEBUG", 0)) {
             std::fprintf(stderr, "serial debug: N %llu L %llu K %llu sigma %.3f: %u iterations (%u "
-                         "stopped short), %llu queued, enqueue %.1f ms, wait %.1f ms\n",
+                         "stopped short), %llu queued, estimate + tables %.1f ms, enqueue %.1f ms, wait %.1f ms\n",
                          (unsigned long long)N, (unsigned long long)L, (unsigned long long)K, sigma,
-                         ctrl[3], ctrl[6], (unsigned long long)queued, t_enqueue, t_wait);
+                         ctrl[3], ctrl[6], (unsigned long long)queued, t_prep, t_enqueue, t_wait);
         }
     }
     HIP_TRY(hipEventRecord(d->sev[1], s));

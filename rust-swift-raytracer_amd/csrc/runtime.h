@@ -63,6 +63,7 @@ struct DeviceState {
     // stream window of a chunk, xorshift jump matrices, control block
     uint32_t *sstates = nullptr;     size_t sstates_cap = 0;
     double *sM = nullptr;            size_t sM_cap = 0;
+    double *sV = nullptr;            size_t sV_cap = 0;     // prefix sums of per-sample variances
     uint32_t *swin = nullptr;        size_t swin_cap = 0;
     uint32_t *sbend = nullptr;       size_t sbend_cap = 0;
     uint32_t *sjump = nullptr;
