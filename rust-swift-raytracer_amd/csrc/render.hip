@@ -775,6 +775,10 @@ void trace_kernel(TraceParams p) {
     bool active = false;
     uint32_t rays = 0, tri_in = 0, sph_tests = 0, node_tests = 0, tnode_tests = 0,
              tri_done = 0;
+    // iteration mix (counting variant, lane 0's view; wave-uniform): loop
+    // iterations, iterations that walked the sphere tree, active lanes summed
+    // over all iterations and over the walking ones (RT_AMD_ITER_DEBUG)
+    uint32_t it_all = 0, it_walk = 0, lanes_all = 0, lanes_walk = 0;
 
     uint32_t pool_next = 0, pool_end = 0;  // wave-uniform job pool
     bool exhausted = false;
@@ -839,6 +843,8 @@ void trace_kernel(TraceParams p) {
         F3 vdir = dir;
         bool renorm = false;
         bool done = false;
+        bool walked = false;  // (kCount: the iteration mix)
+        const uint32_t nact = kCount ? (uint32_t)__popcll(__ballot(active)) : 0u;
         if (active) {
             // ---- ray_color's bounce loop (common.rs:267-282) as a lane state
             // machine: setup -> sphere walk -> triangle walk -> shade.  The walks
@@ -902,6 +908,7 @@ void trace_kernel(TraceParams p) {
                 walk_now = nwalk >= p.walk_min || nother == 0;
             }
             if (kBvh && phase == kSph && walk_now) {
+                walked = true;
                 constexpr uint32_t kEnd = kLds ? 0xFFFFu : kNodeEndDev;
                 const SphBound bnd = sph_bound(p, org);
                 F3 nlo, nhi;
@@ -1067,6 +1074,13 @@ void trace_kernel(TraceParams p) {
                 active = false;
             }
         }
+        if (kCount && nact != 0) {  // (wave-uniform: every lane counts the same)
+            const bool wk = __ballot(walked) != 0;
+            ++it_all;
+            lanes_all += nact;
+            it_walk += wk ? 1u : 0u;
+            lanes_walk += wk ? nact : 0u;
+        }
         const uint64_t dead = __ballot(!active);
         const uint32_t ndead = (uint32_t)__popcll(dead);
         const bool refill = dead != 0 && (ndead >= p.refill_min || ndead == kWave);
@@ -1206,6 +1220,7 @@ void trace_kernel(TraceParams p) {
     // of a multi-GPU tile's overhead); the host sums the records
     if (!kCount || p.stats == nullptr) return;  // (!kCount: the counters compile away)
     uint64_t c[6] = {rays, tri_in, sph_tests, node_tests, tnode_tests, tri_done};
+    const uint64_t mix[4] = {it_all, it_walk, lanes_all, lanes_walk};  // (wave-uniform)
 #pragma unroll
     for (int k = 0; k < 6; ++k)
         for (uint32_t off = kWave / 2; off > 0; off >>= 1) c[k] += __shfl_xor(c[k], (int)off);
@@ -1213,6 +1228,7 @@ void trace_kernel(TraceParams p) {
         unsigned long long *w = p.stats + (size_t)wave_id * kStatSlots;
 #pragma unroll
         for (int k = 0; k < 6; ++k) w[k < 4 ? k : k + 4] += c[k];
+        for (int k = 0; k < 4; ++k) w[10 + k] += mix[k];
 #ifdef RT_STAMPS
         for (int k = 0; k < 4; ++k) w[4 + k] += stamp_acc[k];
 #endif

@@ -649,6 +649,11 @@ int render_frame(WorldState &w, const CameraModel &cam, size_t width, size_t hei
         stats->big_sphere_tests = use_bvh ? st[0] * (uint64_t)d->nbig : st[0] * (uint64_t)d->nsph;
         for (int k = 0; k < 4; ++k) stats->stamp_cycles[k] = st[4 + k];
         stats->tri_node_tests = st[8];
+        if (env_u64("RT_AMD_ITER_DEBUG", 0))
+            std::fprintf(stderr, "iteration mix: %llu iterations (%.1f active lanes), %llu walking (%.1f lanes), "
+                         "%llu other (%.1f lanes)\n", st[10], st[12] / std::max(1.0, (double)st[10]), st[11],
+                         st[13] / std::max(1.0, (double)st[11]), st[10] - st[11],
+                         (st[12] - st[13]) / std::max(1.0, (double)(st[10] - st[11])));
         stats->tri_bvh = use_tbvh ? 1u : 0u;
         stats->fused_resolve = fused ? 1u : 0u;
         stats->primary_lists = primary_lists ? 1u : 0u;
