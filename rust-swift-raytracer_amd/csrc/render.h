@@ -146,6 +146,9 @@ hipError_t launch_serial_window(const uint32_t *ctrl, const uint32_t *jump, uint
 // ctrl (a, the state at a, resolved).  bend: scratch of
 // ceil(L / serial_walk_block(L)) * K u32.
 uint32_t serial_walk_block(uint32_t L);
+// path, fin (optional, both or neither): scratch of ceil(L / R) R K u32 for the
+// block walks' recorded paths and 4 + 256 u32 for the chain's result; with
+// them the full blocks' states are gathered by a parallel kernel, not re-walked.
 // V (optional): the per-sample scatter-count variances as npix + 1 per-pixel
 // prefix sums of spp var followed by npix per-pixel variances; with it
 // the walk sets the next iteration's candidates per sample in ctrl[5] (<= K):
@@ -153,8 +156,8 @@ uint32_t serial_walk_block(uint32_t L);
 // pass and the walks use ctrl[5] when it is set.
 hipError_t launch_serial_walk(uint32_t *ctrl, const float *table, const double *M, const double *V,
                               uint32_t npix, uint32_t spp, float z, float sfloor, const uint32_t *win,
-                              uint32_t *states, uint32_t *bend, uint32_t L, uint32_t K, uint32_t depth,
-                              uint32_t nserial, hipStream_t stream);
+                              uint32_t *states, uint32_t *bend, uint32_t *path, uint32_t *fin, uint32_t L,
+                              uint32_t K, uint32_t depth, uint32_t nserial, hipStream_t stream);
 // inv_spp = 1.0 / (spp as f32) computed from the signed spp (common.rs:345).
 hipError_t launch_resolve_ex(const float *samples, uint32_t *out, uint32_t npix, uint32_t spp,
                              float inv_spp, uint32_t width, uint32_t slab_row0,

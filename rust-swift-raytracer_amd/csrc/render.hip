@@ -1448,9 +1448,13 @@ __device__ __forceinline__ uint32_t serial_k(const uint32_t *ctrl, uint32_t K) {
     return k != 0u && k < K ? k : K;
 }
 
+// path (optional): the offset B at the start of each of the block's samples,
+// sample-major (path[(jl - j0) * nb * K + t], coalesced), so that the states
+// of the true path are a gather (serial_states_kernel), not a re-walk
 __global__ __launch_bounds__(256) void serial_walk_blocks_kernel(
     const uint32_t *__restrict__ ctrl, const float *__restrict__ table, const double *__restrict__ M,
-    uint32_t *__restrict__ bend, uint32_t L, uint32_t K, uint32_t R, uint32_t depth, uint32_t nserial) {
+    uint32_t *__restrict__ bend, uint32_t *__restrict__ path, uint32_t L, uint32_t K, uint32_t R,
+    uint32_t depth, uint32_t nserial) {
     if (ctrl[0] != 0u) return;
     K = serial_k(ctrl, K);
     const uint32_t a = ctrl[4];
@@ -1460,34 +1464,53 @@ __global__ __launch_bounds__(256) void serial_walk_blocks_kernel(
     if (t >= nb * K) return;
     const uint32_t blk = t / K, k0 = t - blk * K;
     const uint32_t j0 = blk * R, j1 = min(j0 + R, n);
+    const size_t stride = (size_t)nb * K;
     uint32_t B = serial_lo(M, a, j0, K, depth, nserial) + k0;
-    for (uint32_t jl = j0; jl < j1 && B != kWalkInvalid; ++jl)
+    for (uint32_t jl = j0; jl < j1 && B != kWalkInvalid; ++jl) {
+        if (path) path[(size_t)(jl - j0) * stride + t] = B;
         B = walk_step(table, M, a, K, depth, nserial, jl, B);
+    }
     bend[t] = B;
 }
 
 __global__ __launch_bounds__(256) void serial_walk_finish_kernel(
     uint32_t *__restrict__ ctrl, const float *__restrict__ table, const double *__restrict__ M,
     const double *__restrict__ V, uint32_t npix, uint32_t spp, const uint32_t *__restrict__ win,
-    const uint32_t *__restrict__ bend, uint32_t *__restrict__ states, uint32_t L, uint32_t Kmax, uint32_t R,
-    uint32_t depth, uint32_t nserial, float z, float sfloor) {
+    const uint32_t *__restrict__ bend, uint32_t *__restrict__ states, uint32_t *__restrict__ fin, uint32_t L,
+    uint32_t Kmax, uint32_t R, uint32_t depth, uint32_t nserial, float z, float sfloor) {
     __shared__ uint32_t bstart[256];
+    __shared__ uint32_t blo[256];
     __shared__ uint32_t nfull;
-    if (ctrl[0] != 0u) return;
+    if (ctrl[0] != 0u) {
+        if (fin && threadIdx.x == 0) fin[1] = 0u;  // (serial_states_kernel: nothing)
+        return;
+    }
     const uint32_t K = serial_k(ctrl, Kmax);
     const uint32_t a = ctrl[4];
     const uint32_t n = min(L, nserial - a);
     const uint32_t nb = (n + R - 1) / R;
+    // every block's window base at once (they do not depend on the path), so
+    // the chain below is one dependent load per block
+    for (uint32_t blk = threadIdx.x; blk < nb; blk += blockDim.x)
+        blo[blk] = serial_lo(M, a, blk * R, K, depth, nserial);
+    __syncthreads();
     if (threadIdx.x == 0) {
         uint32_t B = 0, blk = 0;
         for (; blk < nb; ++blk) {
-            const uint32_t l = serial_lo(M, a, blk * R, K, depth, nserial);
+            const uint32_t l = blo[blk];
             const uint32_t e = (B >= l && B - l < K) ? bend[(size_t)blk * K + (B - l)] : kWalkInvalid;
             if (e == kWalkInvalid) break;
             bstart[blk] = B;
+            if (fin) fin[4 + blk] = blk * K + (B - l);  // the block's path column
             B = e;
         }
         nfull = blk;
+        if (fin) {
+            fin[0] = a;
+            fin[1] = blk;
+            fin[2] = nb * K;
+            fin[3] = n;  // (the last block may be short)
+        }
         uint32_t done = min(blk * R, n);
         if (blk < nb) {
             // the path leaves a window inside this block: resolve it lane-serially
@@ -1527,6 +1550,7 @@ __global__ __launch_bounds__(256) void serial_walk_finish_kernel(
         }
     }
     __syncthreads();
+    if (fin) return;  // the full blocks' states: serial_states_kernel (a gather)
     for (uint32_t blk = threadIdx.x; blk < nfull; blk += blockDim.x) {
         uint32_t B = bstart[blk];
         const uint32_t j1 = min(blk * R + R, n);
@@ -1535,6 +1559,22 @@ __global__ __launch_bounds__(256) void serial_walk_finish_kernel(
             B = walk_step(table, M, a, K, depth, nserial, jl, B);
         }
     }
+}
+
+// The start states of the iteration's full blocks, one thread per sample:
+// the path the block walk recorded for the block's true start (fin, written by
+// serial_walk_finish_kernel: {a, full blocks, path stride, samples of the
+// iteration, column per block}).
+__global__ __launch_bounds__(256) void serial_states_kernel(const uint32_t *__restrict__ fin,
+                                                            const uint32_t *__restrict__ path,
+                                                            const uint32_t *__restrict__ win,
+                                                            uint32_t *__restrict__ states, uint32_t R) {
+    const uint32_t jl = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t nfull = fin[1];
+    if (jl >= nfull * R || jl >= fin[3]) return;
+    const uint32_t blk = jl / R;
+    const uint32_t B = path[(size_t)(jl - blk * R) * fin[2] + fin[4 + blk]];
+    states[fin[0] + jl] = win[2u * jl + 3u * B];
 }
 
 hipError_t launch_serial_window(const uint32_t *ctrl, const uint32_t *jump, uint32_t *win, uint32_t n,
@@ -1553,15 +1593,20 @@ uint32_t serial_walk_block(uint32_t L) {
 
 hipError_t launch_serial_walk(uint32_t *ctrl, const float *table, const double *M, const double *V,
                               uint32_t npix, uint32_t spp, float z, float sfloor, const uint32_t *win,
-                              uint32_t *states, uint32_t *bend, uint32_t L, uint32_t K, uint32_t depth,
-                              uint32_t nserial, hipStream_t stream) {
+                              uint32_t *states, uint32_t *bend, uint32_t *path, uint32_t *fin, uint32_t L,
+                              uint32_t K, uint32_t depth, uint32_t nserial, hipStream_t stream) {
     if (!L) return hipSuccess;
     const uint32_t R = serial_walk_block(L);
     const uint64_t nt = (uint64_t)((L + R - 1) / R) * K;
+    if (!fin) path = nullptr;
     hipLaunchKernelGGL(serial_walk_blocks_kernel, dim3((uint32_t)((nt + 255) / 256)), dim3(256), 0, stream,
-                       ctrl, table, M, bend, L, K, R, depth, nserial);
+                       ctrl, table, M, bend, path, L, K, R, depth, nserial);
     hipLaunchKernelGGL(serial_walk_finish_kernel, dim3(1), dim3(256), 0, stream, ctrl, table, M, V, npix,
-                       spp ? spp : 1u, win, bend, states, L, K, R, depth, nserial, z, sfloor);
+                       spp ? spp : 1u, win, bend, states, path ? fin : nullptr, L, K, R, depth, nserial, z,
+                       sfloor);
+    if (path)
+        hipLaunchKernelGGL(serial_states_kernel, dim3((L + 255) / 256), dim3(256), 0, stream, fin, path, win,
+                           states, R);
     return hipGetLastError();
 }
 

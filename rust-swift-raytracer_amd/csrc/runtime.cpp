@@ -53,7 +53,7 @@ DeviceState::~DeviceState() {
                     bvh_nodes, bvh_prims, big_hot, bvh_miss, bvh_prim_id, big_id, bvh_miss16,
                     sph_shade, sph_kind, tbvh_nodes, tbvh_tris, tbvh_loose,
                     cam_nodes, cam_tris, ptl_off, ptl_items, spl, tile, gath,
-                    sstates, sM, sV, swin, sjump, sctrl, sbend};
+                    sstates, sM, sV, swin, sjump, sctrl, sbend, spath, sfin};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
     for (hipEvent_t e : ev)
@@ -846,6 +846,12 @@ int render_frame_serial(WorldState &w, const CameraModel &cam, size_t width, siz
         }
         HIP_TRY(grow(d->swin, d->swin_cap, wlen));
         HIP_TRY(grow(d->sbend, d->sbend_cap, (L + R_walk - 1) / R_walk * K));
+        // recorded block paths: the states of resolved samples become a gather
+        const bool gather = env_u64("RT_AMD_SERIAL_GATHER", 1) != 0;
+        if (gather) {
+            HIP_TRY(grow(d->spath, d->spath_cap, (L + R_walk - 1) / R_walk * R_walk * K));
+            if (!d->sfin) HIP_TRY(hipMalloc((void **)&d->sfin, (4 + 256) * 4));
+        }
         if (!d->sjump) {
             const std::vector<uint32_t> jt = xorshift_jump_table();
             HIP_TRY(hipMalloc((void **)&d->sjump, jt.size() * 4));
@@ -881,7 +887,8 @@ int render_frame_serial(WorldState &w, const CameraModel &cam, size_t width, siz
                 if (rc) return rc;
                 HIP_TRY(launch_serial_walk(d->sctrl, d->samples, d->sM, adapt ? d->sV : nullptr,
                                            (uint32_t)npix, (uint32_t)spp, (float)z, (float)serial_floor(spp * R),
-                                           d->swin, d->sstates, d->sbend, (uint32_t)L, (uint32_t)K, depth,
+                                           d->swin, d->sstates, d->sbend, gather ? d->spath : nullptr,
+                                           gather ? d->sfin : nullptr, (uint32_t)L, (uint32_t)K, depth,
                                            (uint32_t)N, s));
             }
             const auto t1 = std::chrono::steady_clock::now();

@@ -66,6 +66,8 @@ struct DeviceState {
     double *sV = nullptr;            size_t sV_cap = 0;     // prefix sums of per-sample variances
     uint32_t *swin = nullptr;        size_t swin_cap = 0;
     uint32_t *sbend = nullptr;       size_t sbend_cap = 0;
+    uint32_t *spath = nullptr;       size_t spath_cap = 0;  // block walks' paths (L x K)
+    uint32_t *sfin = nullptr;                               // chain result (4 + 256)
     uint32_t *sjump = nullptr;
     uint32_t *sctrl = nullptr;
     uint32_t *counter = nullptr;                                // job counter
