@@ -69,11 +69,16 @@ def test_serial_narrow_windows_and_short_iterations(monkeypatch):
     """K forced to 24 candidates with 512-sample iterations: paths leave their
     windows after a few samples and each iteration resumes where the last one
     stopped; one-sample iterations; iterations longer than the frame; one K
-    for every iteration (no per-iteration windows from the pixel variances)."""
+    for every iteration (no per-iteration windows from the pixel variances);
+    states re-walked per block instead of gathered from the recorded paths."""
     for env, scene, size in [
         (dict(RT_AMD_SERIAL_K="24", RT_AMD_SERIAL_CHUNK="512"), "c_raytracer_world.txt", (80, 60, 16, 8)),
         (dict(RT_AMD_SERIAL_ADAPT="0"), "c_raytracer_world.txt", (40, 30, 16, 8)),
         (dict(RT_AMD_SERIAL_ADAPT="0", RT_AMD_SERIAL_CHUNK="700"), "world.txt", (33, 17, 3, 8)),
+        # resolved states re-walked per block instead of gathered from the block paths
+        (dict(RT_AMD_SERIAL_GATHER="0"), "c_raytracer_world.txt", (40, 30, 16, 8)),
+        (dict(RT_AMD_SERIAL_GATHER="0", RT_AMD_SERIAL_K="24", RT_AMD_SERIAL_CHUNK="300"), "world.txt",
+         (29, 13, 4, 8)),
         (dict(RT_AMD_SERIAL_CHUNK="1"), "world.txt", (12, 9, 2, 8)),
         (dict(RT_AMD_SERIAL_CHUNK="100"), "world.txt", (13, 7, 3, 8)),
         (dict(RT_AMD_SERIAL_CHUNK="100000", RT_AMD_SERIAL_Z10="5"), "world.txt", (31, 17, 4, 8)),
