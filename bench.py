@@ -179,8 +179,10 @@ def _timed(args, step, stream, sync, barrier):
 def _post_move(world, step, sync, dz=-0.05):
     """Interactive re-render (lib.rs:60-63, GameView.swift:198-219): the frame
     right after move_camera_position, against steady frames of the moved
-    camera.  The moved camera's primary candidate lists / camera tree are
-    built on a host thread meanwhile; the first frame renders without them."""
+    camera.  Sphere scenes build the moved camera's primary candidate lists on
+    the device before the frame (RT_AMD_GPU_LISTS=0: on a host thread while the
+    first frames render without them); triangle scenes rebuild the camera tree
+    and strip lists on the host before the frame."""
     sync()
     world.move_camera(0.0, 0.0, dz)
     t0 = time.perf_counter()

@@ -654,6 +654,31 @@ static bool camera_inverse(const CameraModel &cam, double Mi[3][3]) {
     return true;
 }
 
+bool sphere_list_params(const SphereBVH &bv, const CameraModel &cam, size_t width, size_t height,
+                        SphereListParams &out) {
+    // (the checks and constants of build_primary_sphere_lists below)
+    const size_t n = bv.prims.size() / 4;
+    if (n == 0 || n >= kSphListWalk || width < 2 || height < 2 || height > (1u << 24) ||
+        width > (1u << 24) || width * height > (1ull << 28))
+        return false;
+    const Vec3 cv[4] = {cam.origin, cam.lower_left, cam.horizontal, cam.vertical};
+    double mag = 0;
+    for (const Vec3 &v : cv) mag = std::max({mag, std::fabs((double)v.x), std::fabs((double)v.y),
+                                             std::fabs((double)v.z)});
+    double Mi[3][3];
+    if (!(mag < 1e3) || !camera_inverse(cam, Mi)) return false;
+    for (int r = 0; r < 3; ++r)
+        for (int c = 0; c < 3; ++c) out.Mi[3 * r + c] = Mi[r][c];
+    out.o[0] = cam.origin.x; out.o[1] = cam.origin.y; out.o[2] = cam.origin.z;
+    out.e_abs = 4e-6 * (std::fabs(out.o[0]) + std::fabs(out.o[1]) + std::fabs(out.o[2]) + bv.mag);
+    out.wden = (double)(float)(width - 1);
+    out.hden = (double)(float)(height - 1);
+    out.n = (uint32_t)n;
+    out.width = (uint32_t)width;
+    out.height = (uint32_t)height;
+    return true;
+}
+
 PrimarySphereLists build_primary_sphere_lists(const SphereBVH &bv, const CameraModel &cam,
                                               size_t width, size_t height) {
     PrimarySphereLists out;

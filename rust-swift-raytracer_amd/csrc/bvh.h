@@ -141,5 +141,15 @@ struct PrimarySphereLists {
 };
 PrimarySphereLists build_primary_sphere_lists(const SphereBVH &bv, const CameraModel &cam,
                                               size_t width, size_t height);
+// The same build on the device (render.hip launch_sphere_lists): the host
+// checks and the per-frame constants; false = no lists (every primary ray walks).
+struct SphereListParams {
+    double Mi[9];          // inverse camera map, row-major
+    double o[3];           // camera origin
+    double e_abs, wden, hden;
+    uint32_t n, width, height;
+};
+bool sphere_list_params(const SphereBVH &bv, const CameraModel &cam, size_t width, size_t height,
+                        SphereListParams &out);
 
 }  // namespace rtamd

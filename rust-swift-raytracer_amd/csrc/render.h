@@ -133,6 +133,14 @@ RT_HOST_DEVICE inline uint32_t serial_lo(const double *M, uint32_t a, uint32_t j
 }
 
 hipError_t launch_trace(const TraceParams &p, uint32_t blocks, hipStream_t stream);
+// Primary sphere lists built on the device (bvh.h build_primary_sphere_lists,
+// the same double arithmetic per sphere, then one thread per pixel collecting
+// the spheres whose projected box covers it, in tree order): rec gets 2 u32
+// per pixel; rects (n int4) and flag (1 u32) are scratch.  Mi: 9 doubles,
+// o: 3; every pixel walks when a ball straddles the camera plane.
+hipError_t launch_sphere_lists(const float4 *prims, uint32_t n, const double *Mi, const double *o,
+                               double e_abs, double wden, double hden, uint32_t width, uint32_t height,
+                               int4 *rects, uint32_t *flag, uint2 *rec, hipStream_t stream);
 // SERIAL mode.  ctrl (u32[8]): {resolved, state at sample a, sum of b (low
 // bits), iterations, a = first unresolved sample, candidates per sample of the
 // next iteration (0: the launch's K), iterations that stopped short, 0}.

@@ -135,6 +135,7 @@ constexpr uint32_t kWave = 64;
 constexpr uint32_t kNodeEndDev = 0xFFFFFFFFu;  // bvh.h kNodeEnd
 constexpr uint32_t kLeafBitDev = 0x80000000u;  // bvh.h kLeafBit
 constexpr uint32_t kSphListWalk = 0xFFFFu;     // bvh.h kSphListWalk
+constexpr uint32_t kSphListMaxDev = 3u;        // bvh.h kSphListMax
 constexpr uint32_t kBatch = 8;  // spheres per scalar-load batch (sphere count padded to it)
 
 // ------------------------------------------------------------ sphere stage
@@ -1607,6 +1608,133 @@ hipError_t launch_serial_walk(uint32_t *ctrl, const float *table, const double *
     if (path)
         hipLaunchKernelGGL(serial_states_kernel, dim3((L + 255) / 256), dim3(256), 0, stream, fin, path, win,
                            states, R);
+    return hipGetLastError();
+}
+
+// ------------------------------------------------------------ primary sphere lists
+// Device twin of bvh.cpp build_primary_sphere_lists (same double operations in
+// the same order, -ffp-contract=off): per tree sphere, the box of its inflated
+// ball projected through the inverse camera map to a pixel rectangle (rows
+// counted from the bottom, common.rs:327), empty if behind the camera; flag
+// bit 0: some ball straddles the camera plane or is not finite (every pixel
+// walks).
+struct SplConst { double Mi[9], o[3], e_abs, wden, hden; };
+
+__global__ __launch_bounds__(256) void spl_rect_kernel(const float4 *__restrict__ prims, uint32_t n,
+                                                       SplConst k, uint32_t W, uint32_t H,
+                                                       int4 *__restrict__ rects, uint32_t *__restrict__ flag) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const float4 s = prims[i];
+    const double c[3] = {s.x, s.y, s.z};
+    const double r = sqrt((double)s.w) * (1 + 1e-6);
+    const double a = sqrt((c[0] - k.o[0]) * (c[0] - k.o[0]) + (c[1] - k.o[1]) * (c[1] - k.o[1]) +
+                          (c[2] - k.o[2]) * (c[2] - k.o[2]));
+    const double R = r + 2 * 3e-3 * (a + r) * 1.01 + 2 * k.e_abs;
+    int4 rect = make_int4(1, 0, 1, 0);  // empty
+    if (!isfinite(R) || !isfinite(a)) {
+        atomicOr(flag, 1u);
+        rects[i] = rect;
+        return;
+    }
+    double umin = 1e300, umax = -1e300, vmin = 1e300, vmax = -1e300;
+    int front = 0, behind = 0;
+    for (int q = 0; q < 8; ++q) {
+        const double P[3] = {c[0] + (q & 1 ? R : -R) - k.o[0], c[1] + (q & 2 ? R : -R) - k.o[1],
+                             c[2] + (q & 4 ? R : -R) - k.o[2]};
+        double w[3];
+        for (int t = 0; t < 3; ++t) w[t] = k.Mi[3 * t] * P[0] + k.Mi[3 * t + 1] * P[1] + k.Mi[3 * t + 2] * P[2];
+        const double wn = fabs(w[0]) + fabs(w[1]) + fabs(w[2]);
+        if (w[2] > 1e-6 * wn) {
+            ++front;
+            umin = fmin(umin, w[0] / w[2]); umax = fmax(umax, w[0] / w[2]);
+            vmin = fmin(vmin, w[1] / w[2]); vmax = fmax(vmax, w[1] / w[2]);
+        } else if (w[2] < -1e-6 * wn) {
+            ++behind;
+        }
+    }
+    if (behind != 8 && front < 8) atomicOr(flag, 1u);  // straddles the camera plane
+    if (front == 8) {
+        const double cl = floor(umin * k.wden) - 2, ch = floor(umax * k.wden) + 1;
+        const double rl = floor(vmin * k.hden) - 2, rh = floor(vmax * k.hden) + 1;
+        if (!(ch < 0 || cl > (double)(W - 1) || rh < 0 || rl > (double)(H - 1)))
+            rect = make_int4(cl < 0 ? 0 : (int)cl, ch > (double)(W - 1) ? (int)(W - 1) : (int)ch,
+                             rl < 0 ? 0 : (int)rl, rh > (double)(H - 1) ? (int)(H - 1) : (int)rh);
+    }
+    rects[i] = rect;
+}
+
+// One thread per pixel of a 16 x 16 tile (record row 0 = the top image row):
+// the first three tree spheres whose rectangle covers it, or "walk" past three
+// (bvh.h PrimarySphereLists).  Rectangles are culled against the tile 256 at a
+// time and compacted, in tree order, into LDS; a tile whose pixels have all
+// overflowed stops early.
+__global__ __launch_bounds__(256) void spl_fill_kernel(const int4 *__restrict__ rects, uint32_t n,
+                                                       const uint32_t *__restrict__ flag, uint32_t W, uint32_t H,
+                                                       uint2 *__restrict__ rec) {
+    __shared__ int4 rl[256];
+    __shared__ uint32_t ri[256];
+    __shared__ uint32_t wc[4];
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+    const int col = (int)(blockIdx.x * 16 + (tid & 15u)), row = (int)(blockIdx.y * 16 + (tid >> 4));
+    const bool on = col < (int)W && row < (int)H;
+    const int rb = (int)H - 1 - row;  // counted from the bottom
+    // the tile's extent: columns [tc0, tc1], bottom-counted rows [tr0, tr1]
+    const int tc0 = (int)(blockIdx.x * 16), tc1 = min(tc0 + 15, (int)W - 1);
+    const int tr1 = (int)H - 1 - (int)(blockIdx.y * 16), tr0 = max(tr1 - 15, 0);
+    uint32_t cnt = flag[0] != 0u ? kSphListMaxDev + 1u : 0u, w0 = 0, w1 = 0;
+    for (uint32_t b0 = 0; b0 < n; b0 += 256) {
+        const uint32_t i = b0 + tid;
+        int4 r = make_int4(1, 0, 1, 0);
+        if (i < n) r = rects[i];
+        const bool keep = r.x <= tc1 && r.y >= tc0 && r.z <= tr1 && r.w >= tr0;
+        const uint64_t m = __ballot(keep);
+        if (lane == 0) wc[wave] = (uint32_t)__popcll(m);
+        __syncthreads();
+        uint32_t off = 0, total = 0;
+        for (uint32_t w = 0; w < 4; ++w) {
+            off += w < wave ? wc[w] : 0u;
+            total += wc[w];
+        }
+        if (keep) {
+            const uint32_t pos = off + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                                 __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+            rl[pos] = r;
+            ri[pos] = i;
+        }
+        __syncthreads();
+        for (uint32_t j = 0; j < total && cnt <= kSphListMaxDev; ++j) {
+            const int4 q = rl[j];
+            if (col >= q.x && col <= q.y && rb >= q.z && rb <= q.w) {
+                const uint32_t idx = ri[j];
+                if (cnt == 0) w0 = idx;
+                else if (cnt == 1) w0 |= idx << 16;
+                else if (cnt == 2) w1 = idx;
+                ++cnt;
+            }
+        }
+        if (__syncthreads_and(!on || cnt > kSphListMaxDev)) break;
+    }
+    if (!on) return;
+    const uint32_t c = cnt > kSphListMaxDev ? kSphListWalk : cnt;
+    rec[(size_t)row * W + (uint32_t)col] = make_uint2(w0, (w1 & 0xFFFFu) | (c << 16));
+}
+
+hipError_t launch_sphere_lists(const float4 *prims, uint32_t n, const double *Mi, const double *o,
+                               double e_abs, double wden, double hden, uint32_t width, uint32_t height,
+                               int4 *rects, uint32_t *flag, uint2 *rec, hipStream_t stream) {
+    SplConst k;
+    for (int i = 0; i < 9; ++i) k.Mi[i] = Mi[i];
+    for (int i = 0; i < 3; ++i) k.o[i] = o[i];
+    k.e_abs = e_abs;
+    k.wden = wden;
+    k.hden = hden;
+    hipError_t e = hipMemsetAsync(flag, 0, 4, stream);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(spl_rect_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, prims, n, k, width, height,
+                       rects, flag);
+    hipLaunchKernelGGL(spl_fill_kernel, dim3((width + 15) / 16, (height + 15) / 16), dim3(256), 0, stream, rects, n,
+                       flag, width, height, rec);
     return hipGetLastError();
 }
 

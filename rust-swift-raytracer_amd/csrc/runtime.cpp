@@ -53,7 +53,8 @@ DeviceState::~DeviceState() {
                     bvh_nodes, bvh_prims, big_hot, bvh_miss, bvh_prim_id, big_id, bvh_miss16,
                     sph_shade, sph_kind, tbvh_nodes, tbvh_tris, tbvh_loose,
                     cam_nodes, cam_tris, ptl_off, ptl_items, spl, tile, gath,
-                    sstates, sM, sV, swin, sjump, sctrl, sbend, spath, sfin};
+                    sstates, sM, sV, swin, sjump, sctrl, sbend, spath, sfin,
+                    gspl, gspl_rects, gspl_flag};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
     for (hipEvent_t e : ev)
@@ -212,11 +213,13 @@ void prepare_camera(WorldState &w, const CameraModel &cam) {
     ++w.ctree_version;
 }
 
-// Primary sphere lists for a new camera or frame size are built on a host
-// thread while frames render without them (RT_AMD_SYNC_LISTS=1: built before
-// the frame).  Every frame is bit-identical either way; only the work per
-// primary ray differs (C2: +3 % per frame without them).
+// Primary sphere lists for a new camera or frame size are built on the device
+// on the frame's stream, before its trace kernel (RT_AMD_GPU_LISTS, default 1).
+// With RT_AMD_GPU_LISTS=0 they are built on a host thread while frames render
+// without them (RT_AMD_SYNC_LISTS=1: built before the frame).  Every frame is
+// bit-identical either way; only the work per primary ray differs.
 static bool sync_lists() { return env_u64("RT_AMD_SYNC_LISTS", 0) != 0; }
+static bool gpu_lists() { return env_u64("RT_AMD_GPU_LISTS", 1) != 0; }
 
 template <typename T>
 static bool job_ready(const std::future<T> &f) {
@@ -287,6 +290,46 @@ static hipError_t grow(T *&buf, size_t &cap, size_t n) {
     hipError_t e = hipMalloc((void **)&buf, n * sizeof(T));
     if (e == hipSuccess) cap = n;
     return e;
+}
+
+// The device build of the primary sphere lists for (cam, width, height),
+// enqueued on s when either changed; false = no lists (every primary ray
+// walks).  RT_AMD_SPL_CHECK=1 (tests): compare them with the host build.
+static int device_sphere_lists(WorldState &w, DeviceState *d, const CameraModel &cam, size_t width,
+                               size_t height, hipStream_t s, bool &ok) {
+    if (!(d->gspl_built && d->gspl_w == width && d->gspl_h == height && same_cam(d->gspl_cam, cam))) {
+        SphereListParams sp;
+        d->gspl_ok = sphere_list_params(w.bvh, cam, width, height, sp) && (height + 15) / 16 <= 65535 &&
+                     sp.n == d->nprims;
+        if (d->gspl_ok) {
+            HIP_TRY(grow(d->gspl, d->gspl_cap, width * height));
+            HIP_TRY(grow(d->gspl_rects, d->gspl_rects_cap, (size_t)sp.n));
+            HIP_TRY(grow(d->gspl_flag, d->gspl_flag_cap, 1));
+            HIP_TRY(launch_sphere_lists(d->bvh_prims, sp.n, sp.Mi, sp.o, sp.e_abs, sp.wden, sp.hden, sp.width,
+                                        sp.height, d->gspl_rects, d->gspl_flag, d->gspl, s));
+            if (env_u64("RT_AMD_SPL_CHECK", 0)) {
+                const PrimarySphereLists h = build_primary_sphere_lists(w.bvh, cam, width, height);
+                std::vector<uint32_t> g(2 * width * height);
+                HIP_TRY(hipMemcpyAsync(g.data(), d->gspl, g.size() * 4, hipMemcpyDeviceToHost, s));
+                HIP_TRY(hipStreamSynchronize(s));
+                for (size_t px = 0; px < width * height; ++px) {
+                    const bool same = h.rec.empty() ? (g[2 * px + 1] >> 16) == kSphListWalk
+                                                    : g[2 * px] == h.rec[2 * px] && g[2 * px + 1] == h.rec[2 * px + 1];
+                    if (!same) {
+                        set_error("RT_AMD_SPL_CHECK: device sphere lists differ from the host build at pixel " +
+                                  std::to_string(px));
+                        return -2;
+                    }
+                }
+            }
+        }
+        d->gspl_cam = cam;
+        d->gspl_w = width;
+        d->gspl_h = height;
+        d->gspl_built = true;
+    }
+    ok = d->gspl_ok;
+    return 0;
 }
 
 int render_frame(WorldState &w, const CameraModel &cam, size_t width, size_t height,
@@ -392,8 +435,14 @@ int render_frame(WorldState &w, const CameraModel &cam, size_t width, size_t hei
         p.bvh_r = bv.radius; p.bvh_rmax = bv.rmax; p.bvh_mag = bv.mag;
         p.bvh_inv_rmin = env_u64("RT_AMD_LINEAR_E", 0) ? INFINITY : bv.inv_rmin;
         // sphere-only scenes: primary rays test their pixel's candidates
-        if (d->ntri == 0 && env_u64("RT_AMD_SPHERE_LISTS", 1) != 0 &&
-            prepare_primary_sphere_lists(w, cam, width, height)) {
+        if (d->ntri == 0 && env_u64("RT_AMD_SPHERE_LISTS", 1) != 0 && gpu_lists()) {
+            bool ok = false;
+            rc = device_sphere_lists(w, d, cam, width, height, s, ok);
+            if (rc) return rc;
+            p.spl = ok ? d->gspl : nullptr;
+            primary_lists = ok;
+        } else if (d->ntri == 0 && env_u64("RT_AMD_SPHERE_LISTS", 1) != 0 &&
+                   prepare_primary_sphere_lists(w, cam, width, height)) {
             if (d->spl_version != w.spl_version) {
                 if (d->spl) HIP_TRY(hipFree(d->spl));
                 d->spl = nullptr;

@@ -50,6 +50,13 @@ struct DeviceState {
     uint64_t ptl_version = 0;
     uint2 *spl = nullptr;                                       // primary sphere lists
     uint64_t spl_version = 0;
+    // primary sphere lists built on the device (render.hip launch_sphere_lists)
+    uint2 *gspl = nullptr;           size_t gspl_cap = 0;
+    int4 *gspl_rects = nullptr;      size_t gspl_rects_cap = 0;
+    uint32_t *gspl_flag = nullptr;   size_t gspl_flag_cap = 0;
+    CameraModel gspl_cam{};
+    size_t gspl_w = 0, gspl_h = 0;
+    bool gspl_built = false, gspl_ok = false;
     size_t lds_bytes = 0;                                      // 0: tree not LDS-stageable
     float *samples = nullptr;        size_t samples_cap = 0;   // sample slab (3 planes)
     float *ring = nullptr;           size_t ring_cap = 0;      // per-wave sample rings (fused resolve)

@@ -389,12 +389,17 @@ def test_bvh_matches_oracle_rtow():
     assert gst["rays"] == st["rays"]
 
 
-def test_primary_sphere_lists_follow_camera_and_size(monkeypatch):
+@pytest.mark.parametrize("gpu", ["1", "0"])
+def test_primary_sphere_lists_follow_camera_and_size(monkeypatch, gpu):
     """Primary rays test per-pixel candidate lists built for the camera and
     frame size (bvh.h PrimarySphereLists): after camera moves (one into the
     sphere field, one far off, which falls back to the walk) and at several
-    sizes every sample equals the tree walk's and brute force."""
-    monkeypatch.setenv("RT_AMD_SYNC_LISTS", "1")  # lists built before each frame
+    sizes every sample equals the tree walk's and brute force.  gpu=1: the
+    lists are built on the device, and every list equals the host build's
+    (RT_AMD_SPL_CHECK)."""
+    monkeypatch.setenv("RT_AMD_GPU_LISTS", gpu)
+    monkeypatch.setenv("RT_AMD_SPL_CHECK", gpu)
+    monkeypatch.setenv("RT_AMD_SYNC_LISTS", "1")  # (host build) lists built before each frame
     src = S.rtow()
     world = R.World(src)
     for mv, (w, h) in [((0.0, 0.0, 0.0), (96, 54)), ((0.0, 0.0, 0.0), (57, 31)),
@@ -416,6 +421,36 @@ def test_primary_sphere_lists_follow_camera_and_size(monkeypatch):
         # (lists exist unless some ball straddles the camera plane or the camera
         # is far out: then every pixel walks)
         assert sc["primary_lists"] == 0 and (sb["primary_lists"] == 1 or mv != (0.0, 0.0, 0.0))
+
+
+@pytest.mark.parametrize("case,w,h", [
+    (dict(seed=71, n=3000, spread=8.0, radius=0.12), 203, 117),
+    (dict(seed=72, n=1500, spread=2.0, radius=0.4, dup=300), 160, 90),
+    (dict(seed=73, n=800, spread=30.0, radius=0.02, big=False, cam=(0.0, 0.0, 20.0)), 97, 61),
+])
+def test_device_sphere_lists_many_spheres(monkeypatch, case, w, h):
+    """The device list build (render.hip spl_fill_kernel: tiles, spheres culled
+    256 at a time, early exit when a tile has overflowed) equals the host build
+    list for list on scenes with thousands of spheres, and the frame equals
+    brute force."""
+    monkeypatch.setenv("RT_AMD_SPL_CHECK", "1")
+    src = _random_scene(**case)
+    a, sa, sma, b, sb, smb = _both_modes(src, w, h, 4)
+    assert sb["primary_lists"] == 1
+    assert_bits_equal(b, a, "frame")
+    assert_bits_equal(smb[:, :3], sma[:, :3], "samples")
+
+
+def test_device_sphere_lists_ready_on_the_first_frame():
+    """Built on the device, the lists serve the first frame after every camera
+    move (no host build to wait for)."""
+    world = R.World(S.rtow())
+    for mv in [(0.0, 0.0, 0.0), (0.4, -0.3, 1.0), (-1.0, 0.5, 3.0)]:
+        world.move_camera(*mv)
+        ref, _ = world.render(96, 54, 2, 8, accel=R.ACCEL_BRUTE)
+        out, st = world.render(96, 54, 2, 8)
+        assert st["primary_lists"] == 1
+        assert_bits_equal(out, ref, f"first frame after {mv}")
 
 
 def test_bvh_full_size_c2_equals_brute_force():
@@ -519,13 +554,16 @@ def test_triangle_bvh_edge_frames(w, h, spp, depth):
     assert gst["rays"] == st["rays"]
 
 
-def test_sphere_lists_built_in_the_background_after_camera_moves():
-    """After a camera move (or on a new world) the first frames of a sphere
-    scene render without the primary candidate lists while a host thread
-    builds them (interactive re-render, lib.rs:60-63); the frames after the
-    build use them.  Triangle scenes rebuild their camera tree and strip lists
-    before the frame (parallel host build).  Every frame equals brute force."""
+def test_sphere_lists_built_in_the_background_after_camera_moves(monkeypatch):
+    """RT_AMD_GPU_LISTS=0: after a camera move (or on a new world) the first
+    frames of a sphere scene render without the primary candidate lists while a
+    host thread builds them (interactive re-render, lib.rs:60-63); the frames
+    after the build use them.  Triangle scenes rebuild their camera tree and
+    strip lists before the frame (parallel host build).  Every frame equals
+    brute force."""
     import time
+
+    monkeypatch.setenv("RT_AMD_GPU_LISTS", "0")
 
     for scene in ("rtow", "mesh_soup"):
         src = S.rtow() if scene == "rtow" else _triangle_scene(31, 500, size=1.0, spheres=30, grid=10)
