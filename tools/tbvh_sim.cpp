@@ -13,6 +13,10 @@
 //                     cell centre, widened per ray from it) for depth < D
 //   SIM_HYB_RANGE=1   ... boxes over the whole cell instead (no widening)
 //   SIM_LEVELS=1      share of visits per tree level
+//   SIM_Q8=B,N        16-B nodes in DFS preorder: N>0 u8 boxes and normal boxes
+//                     on per-block frames (B nodes per block; N=3 per-axis
+//                     normal frames), N=0 u16 boxes with one normal box per
+//                     block, N=-1 global grids of SIM_G=box_bits,normal_bits
 //   g++ -O2 -std=c++17 -I../rust-swift-raytracer_amd/csrc tbvh_sim.cpp \
 //       ../rust-swift-raytracer_amd/csrc/{bvh,scene}.cpp -o tbvh_sim
 #include <cmath>
@@ -24,6 +28,8 @@
 #include <algorithm>
 #include <tuple>
 #include <vector>
+#include <limits>
+#include <memory>
 #include <sstream>
 
 #include "bvh.h"
@@ -130,6 +136,232 @@ static float trace(const TriangleBVH &t, V o, V d, Count &c) {
     return best;
 }
 
+// SIM_Q8=B[,N]: 16-B nodes.  The tree in DFS preorder (first child = next
+// node, skip = + subtree size); blocks of B consecutive nodes carry a float
+// frame (box base + step per axis; normal base + step: one for all axes, or
+// per axis with N=3) and every node stores its box and normal box as u8 on its
+// block's frame, rounded outward from the u16 image.  Counts node visits and
+// frame changes (a header load) per ray.
+struct Q8 {
+    int B = 64, N = 1;
+    std::vector<uint8_t> q;       // 12 per node: box lo xyz, hi xyz, nbox lo xyz, hi xyz
+    std::vector<float> hdr;       // 12 per block: base[3] step[3] nbase[3] nstep[3]
+    std::vector<uint32_t> size, leaf_a;  // subtree size; builder word a for leaves (0: internal)
+    std::vector<float> fbox, nun;  // N=0: u16-image box per node, block union of normal boxes
+    std::vector<float> fnb;        // N<0: per-node normal box (global grids, SIM_G)
+    size_t n = 0;
+};
+static float q8_step(float lo, float hi) {
+    if (!(hi > lo)) return std::numeric_limits<float>::min();
+    float s = (float)(((double)hi - lo) / 255.0 * (1 + 1e-6));
+    while (std::fmaf(255.0f, s, lo) < hi) s = std::nextafter(s, INFINITY);
+    return s;
+}
+static uint8_t q8_down(float x, float s, float b) {
+    int q = (int)std::floor(((double)x - b) / s);
+    q = std::min(255, std::max(0, q));
+    while (q > 0 && std::fmaf((float)q, s, b) > x) --q;
+    while (q < 255 && std::fmaf((float)(q + 1), s, b) <= x) ++q;
+    return (uint8_t)q;
+}
+static uint8_t q8_up(float x, float s, float b) {
+    int q = (int)std::ceil(((double)x - b) / s);
+    q = std::min(255, std::max(0, q));
+    while (q < 255 && std::fmaf((float)q, s, b) < x) ++q;
+    while (q > 0 && std::fmaf((float)(q - 1), s, b) >= x) --q;
+    return (uint8_t)q;
+}
+static Q8 make_q8(const TriangleBVH &t, int B, int N) {
+    Q8 o; o.B = B; o.N = N;
+    const size_t n = t.qnodes.size() / 8;
+    std::vector<uint32_t> order;  // preorder -> builder node
+    std::vector<uint32_t> st{0};
+    while (!st.empty()) {
+        const uint32_t i = st.back(); st.pop_back();
+        order.push_back(i);
+        const uint32_t a = t.qnodes[(size_t)i * 8 + 6];
+        if (!(a & kLeafBit)) { const uint32_t c = a & 0x1FFFFFFFu; st.push_back(c + 1); st.push_back(c); }
+    }
+    o.n = order.size();
+    std::vector<uint32_t> pos(n);
+    for (size_t k = 0; k < order.size(); ++k) pos[order[k]] = (uint32_t)k;
+    o.size.assign(o.n, 1);
+    o.leaf_a.assign(o.n, 0);
+    for (size_t k = o.n; k-- > 0;) {
+        const uint32_t a = t.qnodes[(size_t)order[k] * 8 + 6];
+        if (a & kLeafBit) o.leaf_a[k] = a;
+        else { const uint32_t c = a & 0x1FFFFFFFu; o.size[k] = 1 + o.size[pos[c]] + o.size[pos[c + 1]]; }
+    }
+    auto dec = [](uint32_t q, float s, float b) { return std::fmaf((float)q, s, b); };
+    std::vector<float> f(o.n * 12);
+    for (size_t k = 0; k < o.n; ++k) {
+        const uint32_t *w = &t.qnodes[(size_t)order[k] * 8];
+        const uint32_t u[6] = {w[0] & 0xFFFF, w[0] >> 16, w[1] & 0xFFFF, w[1] >> 16, w[2] & 0xFFFF, w[2] >> 16};
+        const uint32_t m[6] = {w[3] & 0xFFFF, w[3] >> 16, w[4] & 0xFFFF, w[4] >> 16, w[5] & 0xFFFF, w[5] >> 16};
+        for (int j = 0; j < 6; ++j) {
+            f[k * 12 + j] = dec(u[j], t.qbox.step[j % 3], t.qbox.base[j % 3]);
+            f[k * 12 + 6 + j] = dec(m[j], t.nstep, t.nbase);
+        }
+    }
+    const size_t nb = (o.n + B - 1) / B;
+    if (N < 0) {  // SIM_G=Bb,Nb: global grids of 2^Bb / 2^Nb steps from the float nodes
+        const char *g = std::getenv("SIM_G");
+        int Bb = 10, Nb = 8;
+        if (g) std::sscanf(g, "%d,%d", &Bb, &Nb);
+        const int mb = (1 << Bb) - 1, mn = (1 << Nb) - 1;
+        auto gstep = [](float lo, float hi, int m) {
+            float st = (float)(((double)hi - lo) / m * (1 + 1e-6));
+            while (std::fmaf((float)m, st, lo) < hi) st = std::nextafter(st, INFINITY);
+            return st;
+        };
+        auto qd = [](float x, float st, float b, int m) {
+            int q = (int)std::floor(((double)x - b) / st); q = std::min(m, std::max(0, q));
+            while (q > 0 && std::fmaf((float)q, st, b) > x) --q;
+            return std::fmaf((float)q, st, b);
+        };
+        auto qu = [](float x, float st, float b, int m) {
+            int q = (int)std::ceil(((double)x - b) / st); q = std::min(m, std::max(0, q));
+            while (q < m && std::fmaf((float)q, st, b) < x) ++q;
+            return std::fmaf((float)q, st, b);
+        };
+        const float *root = &t.nodes[0];
+        float bb[3], bs[3], nlo = 1, nhi = -1;
+        for (int k = 0; k < 3; ++k) { bb[k] = root[k]; bs[k] = gstep(root[k], root[4 + k], mb); }
+        for (size_t i = 0; i < n; ++i)
+            for (int k = 0; k < 3; ++k) {
+                nlo = std::min(nlo, t.nodes[i * 16 + 8 + k]); nhi = std::max(nhi, t.nodes[i * 16 + 12 + k]);
+            }
+        const float ns = gstep(nlo, nhi, mn);
+        o.fbox.resize(o.n * 6);
+        o.fnb.resize(o.n * 6);
+        for (size_t k = 0; k < o.n; ++k) {
+            const float *fn = &t.nodes[(size_t)order[k] * 16];
+            for (int j = 0; j < 3; ++j) {
+                o.fbox[k * 6 + j] = qd(fn[j], bs[j], bb[j], mb);
+                o.fbox[k * 6 + 3 + j] = qu(fn[4 + j], bs[j], bb[j], mb);
+                o.fnb[k * 6 + j] = qd(fn[8 + j], ns, nlo, mn);
+                o.fnb[k * 6 + 3 + j] = qu(fn[12 + j], ns, nlo, mn);
+            }
+        }
+        return o;
+    }
+    if (N == 0) {  // u16 boxes as now, one normal box per block
+        o.fbox.resize(o.n * 6);
+        o.nun.assign(nb * 6, 0);
+        for (size_t b = 0; b < nb; ++b) {
+            float *u = &o.nun[b * 6];
+            for (int j = 0; j < 3; ++j) { u[j] = INFINITY; u[3 + j] = -INFINITY; }
+            for (size_t k = b * B; k < std::min(o.n, (b + 1) * B); ++k)
+                for (int j = 0; j < 3; ++j) {
+                    u[j] = std::min(u[j], f[k * 12 + 6 + j]);
+                    u[3 + j] = std::max(u[3 + j], f[k * 12 + 9 + j]);
+                }
+        }
+        for (size_t k = 0; k < o.n; ++k)
+            for (int j = 0; j < 6; ++j) o.fbox[k * 6 + j] = f[k * 12 + j];
+        return o;
+    }
+    o.hdr.assign(nb * 12, 0);
+    o.q.assign(o.n * 12, 0);
+    for (size_t b = 0; b < nb; ++b) {
+        float lo[6], hi[6];
+        for (int j = 0; j < 6; ++j) { lo[j] = INFINITY; hi[j] = -INFINITY; }
+        for (size_t k = b * B; k < std::min(o.n, (b + 1) * B); ++k)
+            for (int j = 0; j < 3; ++j) {
+                lo[j] = std::min(lo[j], f[k * 12 + j]); hi[j] = std::max(hi[j], f[k * 12 + 3 + j]);
+                lo[3 + j] = std::min(lo[3 + j], f[k * 12 + 6 + j]); hi[3 + j] = std::max(hi[3 + j], f[k * 12 + 9 + j]);
+            }
+        if (N == 1) {
+            const float l = std::min({lo[3], lo[4], lo[5]}), h = std::max({hi[3], hi[4], hi[5]});
+            for (int j = 3; j < 6; ++j) { lo[j] = l; hi[j] = h; }
+        }
+        float *hd = &o.hdr[b * 12];
+        for (int j = 0; j < 3; ++j) {
+            hd[j] = lo[j]; hd[3 + j] = q8_step(lo[j], hi[j]);
+            hd[6 + j] = lo[3 + j]; hd[9 + j] = q8_step(lo[3 + j], hi[3 + j]);
+        }
+        for (size_t k = b * B; k < std::min(o.n, (b + 1) * B); ++k)
+            for (int j = 0; j < 3; ++j) {
+                o.q[k * 12 + j] = q8_down(f[k * 12 + j], hd[3 + j], hd[j]);
+                o.q[k * 12 + 3 + j] = q8_up(f[k * 12 + 3 + j], hd[3 + j], hd[j]);
+                o.q[k * 12 + 6 + j] = q8_down(f[k * 12 + 6 + j], hd[9 + j], hd[6 + j]);
+                o.q[k * 12 + 9 + j] = q8_up(f[k * 12 + 9 + j], hd[9 + j], hd[6 + j]);
+            }
+    }
+    return o;
+}
+static double g_q8_hdr = 0;
+static float trace_q8(const TriangleBVH &t, const Q8 &Q, V o, V d, Count &c) {
+    c.rays += 1;
+    const float onorm = std::fabs(o.x) + std::fabs(o.y) + std::fabs(o.z);
+    const float iv[3] = {1.0f / d.x, 1.0f / d.y, 1.0f / d.z};
+    const float dist = std::fabs(o.x - t.centre[0]) + std::fabs(o.y - t.centre[1]) +
+                       std::fabs(o.z - t.centre[2]) + t.radius + 2 * onorm;
+    const float rho = 1e-5f * (dist + onorm + t.mag);
+    const float ov[3] = {o.x, o.y, o.z};
+    const float dv[3] = {o.x - t.oc[0], o.y - t.oc[1], o.z - t.oc[2]};
+    float best = INFINITY;
+    size_t cur = (size_t)-1;
+    for (size_t i = 0; i < Q.n;) {
+        c.nodes += 1;
+        if (i / Q.B != cur) { cur = i / Q.B; g_q8_hdr += 1; }
+        const float *hd = Q.N > 0 ? &Q.hdr[cur * 12] : nullptr;
+        const uint8_t *q = Q.N > 0 ? &Q.q[i * 12] : nullptr;
+        float sl = 0, sh = 0, n0[3], n1[3], bl[3], bh[3];
+        for (int k = 0; k < 3; ++k) {
+            if (Q.N > 0) {
+                n0[k] = std::fmaf((float)q[6 + k], hd[9 + k], hd[6 + k]);
+                n1[k] = std::fmaf((float)q[9 + k], hd[9 + k], hd[6 + k]);
+                bl[k] = std::fmaf((float)q[k], hd[3 + k], hd[k]);
+                bh[k] = std::fmaf((float)q[3 + k], hd[3 + k], hd[k]);
+            } else if (Q.N < 0) {
+                n0[k] = Q.fnb[i * 6 + k];
+                n1[k] = Q.fnb[i * 6 + 3 + k];
+                bl[k] = Q.fbox[i * 6 + k];
+                bh[k] = Q.fbox[i * 6 + 3 + k];
+            } else {
+                n0[k] = Q.nun[cur * 6 + k];
+                n1[k] = Q.nun[cur * 6 + 3 + k];
+                bl[k] = Q.fbox[i * 6 + k];
+                bh[k] = Q.fbox[i * 6 + 3 + k];
+            }
+            float a = n0[k] * dv[k], b = n1[k] * dv[k];
+            sl += std::fmin(a, b); sh += std::fmax(a, b);
+        }
+        float tn = -INFINITY, tf = INFINITY;
+        for (int k = 0; k < 3; ++k) {
+            float a = sl * n0[k], b = sl * n1[k], cc = sh * n0[k], dd = sh * n1[k];
+            float lo = bl[k] + 2 * std::fmin(std::fmin(a, b), std::fmin(cc, dd)) - rho;
+            float hi = bh[k] + 2 * std::fmax(std::fmax(a, b), std::fmax(cc, dd)) + rho;
+            float t0 = (lo - ov[k]) * iv[k], t1 = (hi - ov[k]) * iv[k];
+            tn = std::fmax(tn, std::fmin(t0, t1));
+            tf = std::fmin(tf, std::fmax(t0, t1));
+        }
+        const bool skip = tn > tf || tf < 0.001f || tn > best;
+        const uint32_t a = Q.leaf_a[i];
+        if (!skip && a) {
+            const uint32_t first = (a & ~kLeafBit) >> 3, count = a & 7u;
+            for (uint32_t j = first; j < first + count; ++j) {
+                c.tests += 1;
+                const float *r = &t.tris[(size_t)j * 16];
+                V N{r[0], r[1], r[2]};
+                float cs = dot(N, d);
+                if (std::fabs(cs) < 1e-8f) continue;
+                float tt = (dot(N, o) + r[3]) / cs;
+                if (tt < 0.001f || tt > best) continue;
+                V pp = add(o, mul(d, tt));
+                V v0{r[4], r[5], r[6]}, v1{r[8], r[9], r[10]}, v2{r[12], r[13], r[14]};
+                if (dot(N, cross(sub(v1, v0), sub(pp, v0))) < 0) continue;
+                if (dot(N, cross(sub(v2, v1), sub(pp, v1))) < 0) continue;
+                if (dot(N, cross(sub(v0, v2), sub(pp, v2))) < 0) continue;
+                best = tt;
+            }
+        }
+        i = skip ? i + Q.size[i] : i + 1;
+    }
+    return best;
+}
+
 int main(int argc, char **argv) {
     if (argc < 2) { std::fprintf(stderr, "usage: tbvh_sim scene.txt [W H]\n"); return 2; }
     std::ifstream f(argv[1]);
@@ -178,7 +410,14 @@ int main(int argc, char **argv) {
         std::printf("exact phantom tree: nodes %zu\n", t.nodes.size() / 16);
     }
     V org{cm.origin.x, cm.origin.y, cm.origin.z};
-    Count prim, sec;
+    Count prim, sec, q8c;
+    std::unique_ptr<Q8> q8;
+    size_t q8diff = 0;
+    if (const char *qs = std::getenv("SIM_Q8")) {
+        int B = 64, N = 1;
+        std::sscanf(qs, "%d,%d", &B, &N);
+        q8 = std::make_unique<Q8>(make_q8(t, B, N));
+    }
     uint32_t rng = 2547549u;
     auto rnd = [&]() { rng ^= rng << 13; rng ^= rng >> 17; rng ^= rng << 5; return rng * 0x1p-32f; };
     int hits = 0;
@@ -193,7 +432,11 @@ int main(int argc, char **argv) {
                 ++hits;
                 V o2 = add(org, mul(d, tt));
                 V d2 = unit(V{rnd() * 2 - 1, rnd() * 2 - 1, rnd() * 2 - 1});
-                trace(t, o2, d2, sec);
+                const float t2 = trace(t, o2, d2, sec);
+                if (q8) {
+                    const float t3 = trace_q8(t, *q8, o2, d2, q8c);
+                    if (!(t2 == t3 || (std::isinf(t2) && std::isinf(t3)))) ++q8diff;
+                }
             }
         }
     if (const char *hs = std::getenv("SIM_HYB")) {
@@ -321,6 +564,9 @@ int main(int argc, char **argv) {
     if (sec.rays)
         std::printf("secondary: %.0f rays, %.1f nodes/ray, %.1f tests/ray\n", sec.rays,
                     sec.nodes / sec.rays, sec.tests / sec.rays);
+    if (q8)
+        std::printf("q8 B=%d N=%d: secondary %.1f nodes/ray, %.2f frame changes/ray, %.1f tests/ray, %zu hits differ\n",
+                    q8->B, q8->N, q8c.nodes / q8c.rays, g_q8_hdr / q8c.rays, q8c.tests / q8c.rays, q8diff);
     if (!g_level_visits.empty()) {  // cumulative share of visits in the top levels
         double tot = 0, acc = 0;
         std::vector<size_t> per_level(64, 0);
