@@ -15,6 +15,7 @@
 // relative to raytracer/src/ of Naxaes/Rust-Swift-Raytracer.
 
 #include "rt_oracle.h"
+#include "../rust-swift-raytracer_amd/csrc/unicode_alnum.h"
 
 #include <clocale>
 #include <cmath>
@@ -329,20 +330,17 @@ bool is_ws(uint32_t c) {
            (c >= 0x2000 && c <= 0x200A) || c == 0x2028 || c == 0x2029 || c == 0x202F ||
            c == 0x205F || c == 0x3000;
 }
-// char::is_alphanumeric: exact for ASCII and Latin-1; above U+00FF every code
-// point except whitespace, General Punctuation and CJK punctuation is taken as
-// alphanumeric (approximation of the Unicode tables, documented in DESIGN.md).
+// char::is_alphanumeric (parser.rs:60): Alphabetic || Nd/Nl/No, Unicode
+// 13.0.0.  The ranges are Unicode data (tools/gen_unicode_alnum.py, from perl's
+// unicore Alphabetic table and Python's unicodedata), shared with the product;
+// tests/test_parser.py checks both parsers against those sources directly.
 bool is_alnum(uint32_t c) {
     if (c < 0x80) return (c >= '0' && c <= '9') || (c >= 'a' && c <= 'z') || (c >= 'A' && c <= 'Z');
-    if (c <= 0xFF) {
-        if (c == 0xAA || c == 0xB5 || c == 0xBA || c == 0xB2 || c == 0xB3 || c == 0xB9) return true;
-        if (c >= 0xBC && c <= 0xBE) return true;
-        return c >= 0xC0 && c != 0xD7 && c != 0xF7;
+    for (uint32_t i = 0; i < rtamd::kAlnumRangeCount; ++i) {  // linear: the oracle favours plainness
+        if (c < rtamd::kAlnumRanges[i][0]) return false;
+        if (c <= rtamd::kAlnumRanges[i][1]) return true;
     }
-    if (is_ws(c)) return false;
-    if (c >= 0x2000 && c <= 0x206F) return false;
-    if (c >= 0x3000 && c <= 0x303F) return false;
-    return true;
+    return false;
 }
 
 // A cursor over the (NUL-terminated) source, mirroring the &str slices.

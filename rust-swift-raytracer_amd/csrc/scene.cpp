@@ -11,6 +11,7 @@
 // Built with -ffp-contract=off: the triangle constants precomputed here must
 // carry the exact bits the reference computes per test (common.rs:131-140).
 #include "scene.h"
+#include "unicode_alnum.h"
 
 #include <cmath>
 #include <cstdlib>
@@ -50,19 +51,19 @@ bool unicode_space(uint32_t c) {
     return c == 0x85 || c == 0xA0 || c == 0x1680 || (c >= 0x2000 && c <= 0x200A) ||
            c == 0x2028 || c == 0x2029 || c == 0x202F || c == 0x205F || c == 0x3000;
 }
-// Exact for ASCII and Latin-1; above U+00FF an approximation.
+// char::is_alphanumeric (parser.rs:60): the Unicode 13.0.0 table of
+// unicode_alnum.h (tools/gen_unicode_alnum.py), binary search above ASCII.
 bool unicode_alnum(uint32_t c) {
     if (c < 0x80) {
         return (c >= '0' && c <= '9') || ((c | 0x20) >= 'a' && (c | 0x20) <= 'z');
     }
-    if (c < 0x100) {
-        switch (c) {
-        case 0xAA: case 0xB2: case 0xB3: case 0xB5: case 0xB9: case 0xBA:
-        case 0xBC: case 0xBD: case 0xBE: return true;
-        default: return c >= 0xC0 && c != 0xD7 && c != 0xF7;
-        }
+    uint32_t lo = 0, hi = kAlnumRangeCount;  // first range with end >= c
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) / 2;
+        if (kAlnumRanges[mid][1] < c) lo = mid + 1;
+        else hi = mid;
     }
-    return !unicode_space(c) && !(c >= 0x2000 && c <= 0x206F) && !(c >= 0x3000 && c <= 0x303F);
+    return lo < kAlnumRangeCount && kAlnumRanges[lo][0] <= c;
 }
 
 // A scanner whose position plays the role of the reference's `&str` rest.

@@ -102,3 +102,48 @@ def test_move_camera_matches_reference_formula():
         O.lib().ro_camera_move(O.fptr(s.camera()), d[0], d[1], d[2], O.fptr(cam))
         s.set_camera(cam)
         assert np.array_equal(w.camera().view(np.uint32), cam.view(np.uint32))
+
+
+def _unicode_alnum_truth():
+    """char::is_alphanumeric from the Unicode 13.0.0 sources in this image,
+    computed here independently of the product and oracle tables: perl's
+    Alphabetic inversion list and Python's unicodedata numeric categories."""
+    import glob
+    import unicodedata
+
+    paths = sorted(glob.glob("/usr/share/perl/*/unicore/lib/Alpha/Y.pl"))
+    if not paths or unicodedata.unidata_version != "13.0.0":
+        pytest.skip("Unicode 13.0.0 sources not present")
+    body = open(paths[-1]).read().split("return <<'END';", 1)[1].split("END", 1)[0].split()
+    pts = [int(x) for x in body[1:]]
+    inv = pts + ([0x110000] if len(pts) % 2 else [])
+    import bisect
+
+    def truth(c):
+        alpha = bisect.bisect_right(inv, c) % 2 == 1
+        return alpha or unicodedata.category(chr(c)) in ("Nd", "Nl", "No")
+    return truth, inv
+
+
+def test_identifier_characters_follow_unicode_alphanumeric():
+    """Identifiers run while char::is_alphanumeric || '_' (parser.rs:60): a
+    material name 'M<c>x' parses iff c is alphanumeric -- checked for both
+    parsers at every Alphabetic range boundary (+-1), at the Latin-1 block and
+    at 1500 random code points (surrogates excluded: not chars)."""
+    truth, inv = _unicode_alnum_truth()
+    rng = np.random.default_rng(7)
+    cps = set(range(0x80, 0x100))
+    for b in inv:
+        cps.update((b - 1, b))
+    cps.update(int(x) for x in rng.integers(0x80, 0x110000, 1500))
+    cps = sorted(c for c in cps if 0x80 <= c < 0x110000 and not 0xD800 <= c <= 0xDFFF)
+    bad = []
+    for c in cps:
+        name = "M" + chr(c) + "x"
+        src = (CAM + f"material {name} : Diffuse color 0.5 0.5 0.5;\n"
+               f"sphere center 0.0 0.0 -1.0 radius 0.5 material {name};")
+        w, perr, s, oerr = parse_both(src)
+        want = truth(c)
+        if (perr is None) != want or (oerr is None) != want:
+            bad.append((hex(c), want, perr, oerr))
+    assert not bad, bad[:10]
