@@ -97,7 +97,7 @@ typedef struct RtRenderStats {
   uint32_t primary_lists;    /* 1: primary rays used per-pixel / per-strip
                                 candidate lists (0 right after a camera move or
                                 resize while they are built on a host thread) */
-  uint32_t camera_tree;      /* 1: bounce-0 triangle rays used the camera tree */
+  uint32_t camera_tree;      /* 1: bounce-0 triangle rays used the camera-origin records (tree or strip lists) */
 } RtRenderStats;
 
 /* spp 16, depth 8 (lib.rs:51), SERIAL, seed 2547549, one rank, device -1,

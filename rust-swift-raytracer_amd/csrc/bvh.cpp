@@ -494,7 +494,7 @@ TriangleBVH build_triangle_bvh(const std::vector<Triangle> &tris, const std::vec
 
 CameraTriangleBVH build_camera_triangle_bvh(const std::vector<Triangle> &tris,
                                             const std::vector<float> &tri_hot, const TriangleBVH &tb,
-                                            const float origin[3], uint32_t leaf_size) {
+                                            const float origin[3], uint32_t leaf_size, bool tree) {
     CameraTriangleBVH out;
     for (int k = 0; k < 3; ++k) out.origin[k] = origin[k];
     if (tb.nodes.empty()) return out;
@@ -519,6 +519,19 @@ CameraTriangleBVH build_camera_triangle_bvh(const std::vector<Triangle> &tris,
         prims.push_back(p);
     }
     if (prims.empty()) return out;
+    auto record_boxes = [&]() {
+        out.rec_box.resize(prims.size() * 6);
+        for (size_t i = 0; i < prims.size(); ++i)
+            for (int k = 0; k < 3; ++k) {
+                out.rec_box[i * 6 + k] = down(prims[i].box.lo[k]);
+                out.rec_box[i * 6 + 3 + k] = up(prims[i].box.hi[k]);
+            }
+    };
+    if (!tree) {  // records only (any order: candidates merge by (t, index))
+        out.tris = triangle_records(prims, tris, tri_hot);
+        record_boxes();
+        return out;
+    }
     Builder b(prims, std::min(7u, std::max(1u, leaf_size)));  // count: 3 bits
     b.build_root((uint32_t)prims.size());
     out.depth = b.max_depth;
@@ -534,12 +547,7 @@ CameraTriangleBVH build_camera_triangle_bvh(const std::vector<Triangle> &tris,
     for (uint32_t oct = 0; oct < 8; ++oct) b.links(0, kNodeEnd, oct, out.miss);
     out.tris = triangle_records(prims, tris, tri_hot);
     quantize_boxes(out.nodes, 8, false, out.miss, out.qnodes, out.qbox, nullptr, nullptr);
-    out.rec_box.resize(prims.size() * 6);
-    for (size_t i = 0; i < prims.size(); ++i)
-        for (int k = 0; k < 3; ++k) {
-            out.rec_box[i * 6 + k] = down(prims[i].box.lo[k]);
-            out.rec_box[i * 6 + 3 + k] = up(prims[i].box.hi[k]);
-        }
+    record_boxes();
     return out;
 }
 

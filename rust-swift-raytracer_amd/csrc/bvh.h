@@ -100,9 +100,11 @@ struct CameraTriangleBVH {
     QuantGrid qbox;
     std::vector<float> rec_box;     // per record (tris order): padded phantom box lo.xyz, hi.xyz
 };
+// tree = false: the records and rec_box only (triangle order, no nodes), all
+// the primary strip lists need; bounce-0 rays then never walk this tree.
 CameraTriangleBVH build_camera_triangle_bvh(const std::vector<Triangle> &tris,
                                             const std::vector<float> &tri_hot, const TriangleBVH &tb,
-                                            const float origin[3], uint32_t leaf_size);
+                                            const float origin[3], uint32_t leaf_size, bool tree = true);
 
 // Primary-ray triangle lists.  A bounce-0 ray of pixel (col, row) starts at
 // the camera origin o and points into the pixel's footprint, u in

@@ -935,7 +935,9 @@ void trace_kernel(TraceParams p) {
                 } else if (p.tnodes != 0) {
                     const bool cam = bounce == 0 && p.cam_nnodes != 0;
                     if (tri_begin(p, org, dir, best_t, cam, e, tri_t, tri_i, tri_in, tri_done)) {
-                        if (cam && p.ptl_off != nullptr) {
+                        // (the lists index the camera-origin records, which exist
+                        // without the camera tree's nodes: runtime.cpp prepare_camera)
+                        if (bounce == 0 && p.ptl_off != nullptr) {
                             tri_primary_list<kSerial>(p, lane_job(slot), org, dir, best_t, tri_t, tri_i, tri_in,
                                              tri_done);
                         } else {

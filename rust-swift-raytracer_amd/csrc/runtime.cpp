@@ -205,11 +205,16 @@ static uint32_t cam_leaf() {
     return (uint32_t)env_u64("RT_AMD_CAM_LEAF", 2);  // triangles per camera-tree leaf
 }
 
-void prepare_camera(WorldState &w, const CameraModel &cam) {
+// The camera-origin phantom records (and, with tree, the camera tree over
+// them) for cam's origin.  Frames with primary strip lists need only the
+// records: the lists replace every bounce-0 walk (C5: ~3 ms instead of the
+// tree's ~50 ms after a camera move).
+void prepare_camera(WorldState &w, const CameraModel &cam, bool tree) {
     if (w.tbvh.nodes.empty() || env_u64("RT_AMD_CAMERA_TREE", 1) == 0) return;
     const float o[3] = {cam.origin.x, cam.origin.y, cam.origin.z};
-    if (w.ctree_version && std::memcmp(o, w.ctree.origin, sizeof(o)) == 0) return;
-    w.ctree = build_camera_triangle_bvh(w.scene.triangles, w.packed.tri_hot, w.tbvh, o, cam_leaf());
+    if (w.ctree_version && std::memcmp(o, w.ctree.origin, sizeof(o)) == 0 && (w.ctree_full || !tree)) return;
+    w.ctree = build_camera_triangle_bvh(w.scene.triangles, w.packed.tri_hot, w.tbvh, o, cam_leaf(), tree);
+    w.ctree_full = tree;
     ++w.ctree_version;
 }
 
@@ -237,7 +242,7 @@ static bool same_cam(const CameraModel &a, const CameraModel &b) {
 // rebuild takes ~50 + 6 ms (subtrees built on 16 host threads, bvh.cpp).
 static void prepare_camera_lists(WorldState &w, const CameraModel &cam, size_t width, size_t height,
                                  bool lists) {
-    prepare_camera(w, cam);
+    prepare_camera(w, cam, !lists);
     if (!lists || !w.ctree_version) return;
     if (w.ptl_version && w.ptl_w == width && w.ptl_h == height && w.ptl_ctree == w.ctree_version &&
         same_cam(w.ptl_cam, cam))
@@ -467,19 +472,24 @@ int render_frame(WorldState &w, const CameraModel &cam, size_t width, size_t hei
         d->cam_tris = nullptr;
         d->cam_nnodes = 0;
         const CameraTriangleBVH &ct = w.ctree;
+        if (!ct.tris.empty()) {
+            HIP_TRY(hipMalloc((void **)&d->cam_tris, ct.tris.size() * 4));
+            HIP_TRY(hipMemcpy(d->cam_tris, ct.tris.data(), ct.tris.size() * 4, hipMemcpyHostToDevice));
+        }
         if (!ct.nodes.empty()) {
             HIP_TRY(hipMalloc((void **)&d->cam_nodes, ct.qnodes.size() * 4));
             HIP_TRY(hipMemcpy(d->cam_nodes, ct.qnodes.data(), ct.qnodes.size() * 4, hipMemcpyHostToDevice));
-            HIP_TRY(hipMalloc((void **)&d->cam_tris, ct.tris.size() * 4));
-            HIP_TRY(hipMemcpy(d->cam_tris, ct.tris.data(), ct.tris.size() * 4, hipMemcpyHostToDevice));
             d->cam_nnodes = (uint32_t)(ct.qnodes.size() / 8);
         }
         d->cam_version = w.ctree_version;
     }
     if (use_tbvh) {
-        if (d->cam_nnodes && std::memcmp(w.ctree.origin, &cam.origin, 12) == 0) {
-            p.cam_nodes = d->cam_nodes; p.cam_tris = d->cam_tris;
-            p.cam_nnodes = d->cam_nnodes;
+        if (d->cam_tris && std::memcmp(w.ctree.origin, &cam.origin, 12) == 0) {
+            p.cam_tris = d->cam_tris;
+            if (d->cam_nnodes) {
+                p.cam_nodes = d->cam_nodes;
+                p.cam_nnodes = d->cam_nnodes;
+            }
             if (want_ptl && w.ptl_version && w.ptl_w == width && w.ptl_h == height &&
                 w.ptl_ctree == w.ctree_version && same_cam(w.ptl_cam, cam)) {
                 if (d->ptl_version != w.ptl_version) {
@@ -706,7 +716,7 @@ int render_frame(WorldState &w, const CameraModel &cam, size_t width, size_t hei
         stats->tri_bvh = use_tbvh ? 1u : 0u;
         stats->fused_resolve = fused ? 1u : 0u;
         stats->primary_lists = primary_lists ? 1u : 0u;
-        stats->camera_tree = p.cam_nnodes != 0 ? 1u : 0u;
+        stats->camera_tree = p.cam_tris != nullptr ? 1u : 0u;  // camera-origin records (tree or lists)
         stats->bvh_tri_tests = use_tbvh ? st[9] : stats->tri_tests;
     }
     return 0;

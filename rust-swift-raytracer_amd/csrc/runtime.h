@@ -96,6 +96,7 @@ struct WorldState {
     TriangleBVH tbvh;
     CameraTriangleBVH ctree;      // for the camera origin of ctree_version
     uint64_t ctree_version = 0;   // 0: none built
+    bool ctree_full = false;      // ctree has its nodes (else records only)
     PrimaryTriLists ptl;          // for ptl_cam at ptl_w x ptl_h (and ctree_version)
     CameraModel ptl_cam{};
     size_t ptl_w = 0, ptl_h = 0;
@@ -165,7 +166,7 @@ int render_frame_host(WorldState &w, const CameraModel &cam, size_t width, size_
 
 // (Re)builds the camera-origin triangle tree when the origin changed
 // (load_world, move_camera_position, or a render with another camera).
-void prepare_camera(WorldState &w, const CameraModel &cam);
+void prepare_camera(WorldState &w, const CameraModel &cam, bool tree = false);
 
 long read_samples(WorldState &w, int device, float *out, size_t n);
 

@@ -505,10 +505,14 @@ def test_triangle_bvh_c5_equals_brute_force():
     assert sa["rays"] == sb["rays"]
 
 
-def test_triangle_camera_tree_follows_camera_moves(monkeypatch):
-    """Bounce-0 rays use a tree built for the camera origin; moving the camera
-    must rebuild it (every sample still equals brute force)."""
+@pytest.mark.parametrize("lists", ["1", "0"])
+def test_triangle_camera_tree_follows_camera_moves(monkeypatch, lists):
+    """Bounce-0 rays use the phantom records of the camera origin -- through
+    the primary strip lists (lists=1: records only, no tree) or the camera
+    tree (lists=0); moving the camera must rebuild them (every sample still
+    equals brute force)."""
     monkeypatch.setenv("RT_AMD_SYNC_LISTS", "1")  # tree built before each frame
+    monkeypatch.setenv("RT_AMD_PRIMARY_LISTS", lists)
     src = _triangle_scene(31, 500, size=1.0, spheres=30, grid=10)
     world = R.World(src)
     for mv in [(0.0, 0.0, 0.0), (0.5, -0.25, 1.0), (-3.0, 2.0, -4.0), (0.0, 0.0, 0.0)]:
