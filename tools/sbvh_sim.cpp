@@ -7,7 +7,8 @@
 // Not product code, not a parity check (double arithmetic, no inflation).
 //   g++ -O2 -std=c++17 -I../rust-swift-raytracer_amd/csrc sbvh_sim.cpp \
 //       ../rust-swift-raytracer_amd/csrc/{bvh,scene}.cpp -o sbvh_sim -lpthread
-//   ./sbvh_sim ../scenes/rtow.txt [W H]     (RT_AMD_LEAF: leaf size, default 3)
+//   ./sbvh_sim ../scenes/rtow.txt [W H]     (RT_AMD_LEAF: leaf size, default 3;
+//   SIM_BVH4=1: node fetches and box tests of the tree collapsed to 4-wide nodes)
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
@@ -74,6 +75,69 @@ static int walk(const SphereBVH &b, const std::vector<float> &hot, V o, V d, Hit
     return visits;
 }
 
+// SIM_BVH4=1: the same tree collapsed to 4 children per node (each internal
+// child replaced by its two children), walked with a stack, nearest child
+// first.  Returns node fetches; box tests (children tested) go to *tests.
+static int walk4(const SphereBVH &b, const std::vector<float> &hot, V o, V d, Hit &h, int *tests) {
+    for (uint32_t i : b.big) {
+        const double t = sphere_t(o, d, &hot[(size_t)i * 4]);
+        if (t < h.t) { h.t = t; h.id = (int)i; }
+    }
+    const double inv[3] = {1 / d.x, 1 / d.y, 1 / d.z}, ov[3] = {o.x, o.y, o.z};
+    auto box = [&](uint32_t n, double &tn) {
+        const float *f = &b.nodes[(size_t)n * 8];
+        double a = -INFINITY, z = INFINITY;
+        for (int k = 0; k < 3; ++k) {
+            const double t0 = (f[k] - ov[k]) * inv[k], t1 = (f[4 + k] - ov[k]) * inv[k];
+            a = std::max(a, std::min(t0, t1));
+            z = std::min(z, std::max(t0, t1));
+        }
+        tn = a;
+        return !(a > z || z < 1e-3 || a > h.t);
+    };
+    auto word = [&](uint32_t n, int k) { uint32_t w; std::memcpy(&w, &b.nodes[(size_t)n * 8 + k], 4); return w; };
+    auto leaf = [&](uint32_t n) {
+        const uint32_t a = word(n, 3), cnt = word(n, 7);
+        for (uint32_t j = a & ~kLeafBit; j < (a & ~kLeafBit) + cnt; ++j) {
+            const double t = sphere_t(o, d, &b.prims[(size_t)j * 4]);
+            if (t < h.t) { h.t = t; h.id = (int)b.prim_id[j]; }
+        }
+    };
+    int fetches = 0;
+    double t0;
+    std::vector<std::pair<double, uint32_t>> st;
+    if (!box(0, t0)) return 0;
+    if (word(0, 3) & kLeafBit) { leaf(0); return 1; }
+    st.push_back({t0, 0});
+    while (!st.empty()) {
+        auto [tn, n] = st.back();
+        st.pop_back();
+        if (tn > h.t) continue;
+        ++fetches;
+        uint32_t kids[4], nk = 0;
+        const uint32_t a = word(n, 3);
+        for (uint32_t c = a; c < a + 2; ++c) {
+            if (word(c, 3) & kLeafBit) kids[nk++] = c;
+            else { const uint32_t g = word(c, 3); kids[nk++] = g; kids[nk++] = g + 1; }
+        }
+        std::pair<double, uint32_t> hit[4];
+        int nh = 0;
+        for (uint32_t k = 0; k < nk; ++k) {
+            ++*tests;
+            double t;
+            if (box(kids[k], t)) hit[nh++] = {t, kids[k]};
+        }
+        std::sort(hit, hit + nh, [](auto &x, auto &y) { return x.first > y.first; });  // nearest last
+        for (int k = 0; k < nh; ++k) {
+            if (word(hit[k].second, 3) & kLeafBit) continue;
+            st.push_back(hit[k]);
+        }
+        for (int k = nh - 1; k >= 0; --k)  // leaves now, nearest first
+            if (word(hit[k].second, 3) & kLeafBit) leaf(hit[k].second);
+    }
+    return fetches;
+}
+
 int main(int argc, char **argv) {
     if (argc < 2) { std::fprintf(stderr, "usage: sbvh_sim scene.txt [W H]\n"); return 2; }
     std::ifstream f(argv[1]);
@@ -94,6 +158,8 @@ int main(int argc, char **argv) {
     uint32_t rng = 2547549u;
     auto rnd = [&]() { rng ^= rng << 13; rng ^= rng >> 17; rng ^= rng << 5; return rng * 0x1p-32; };
     std::vector<int> vis[3];  // bounce 0, 1, 2
+    const bool bvh4 = std::getenv("SIM_BVH4") != nullptr;
+    std::vector<int> box4[3];  // SIM_BVH4: children tested per walk
     for (int j = 0; j < H; ++j)
         for (int i = 0; i < W; ++i) {
             const double u = (i + rnd()) / (W - 1), v = (j + rnd()) / (H - 1);
@@ -103,7 +169,14 @@ int main(int argc, char **argv) {
                                mul(V{cm.vertical.x, cm.vertical.y, cm.vertical.z}, v)), o));
             for (int bounce = 0; bounce < 3; ++bounce) {
                 Hit h;
-                vis[bounce].push_back(walk(b, hot, o, d, h));
+                if (bvh4) {
+                    Hit h2;
+                    int tests = 0;
+                    vis[bounce].push_back(walk4(b, hot, o, d, h2, &tests));
+                    box4[bounce].push_back(tests);
+                }
+                const int v2 = walk(b, hot, o, d, h);
+                if (!bvh4) vis[bounce].push_back(v2);
                 if (h.id < 0) break;
                 const float *c = &hot[(size_t)h.id * 4];
                 const V p = add(o, mul(d, h.t));
@@ -127,6 +200,14 @@ int main(int argc, char **argv) {
         std::vector<int> sh = v;
         for (size_t i = sh.size() - 1; i > 0; --i) std::swap(sh[i], sh[(size_t)(rnd() * (i + 1)) % (i + 1)]);
         for (size_t g = 0; g < ng; ++g) rmax += *std::max_element(sh.begin() + g * 64, sh.begin() + g * 64 + 64);
+        if (bvh4 && !box4[k].empty()) {
+            double bt = 0, bmax = 0;
+            for (int x : box4[k]) bt += x;
+            for (size_t g = 0; g < ng; ++g)
+                bmax += *std::max_element(box4[k].begin() + g * 64, box4[k].begin() + g * 64 + 64);
+            std::printf("bvh4 bounce %d: box tests mean %.1f, E[max of 64] %.1f\n", k, bt / box4[k].size(),
+                        ng ? bmax / ng : 0.0);
+        }
         std::sort(v.begin(), v.end());
         std::printf("bounce %d: %zu walks, mean %.1f, p50 %d p90 %d p99 %d max %d; E[max of 64] "
                     "neighbours %.1f, shuffled %.1f (lane use %.0f%% / %.0f%%)\n",
