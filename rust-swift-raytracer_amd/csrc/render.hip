@@ -1621,6 +1621,8 @@ hipError_t launch_serial_walk(uint32_t *ctrl, const float *table, const double *
 // bit 0: some ball straddles the camera plane or is not finite (every pixel
 // walks).
 struct SplConst { double Mi[9], o[3], e_abs, wden, hden; };
+// an empty rectangle that every tile culls (lo above any pixel, hi below)
+__device__ __forceinline__ int4 spl_empty() { return make_int4(0x7FFFFFFF, -1, 0x7FFFFFFF, -1); }
 
 __global__ __launch_bounds__(256) void spl_rect_kernel(const float4 *__restrict__ prims, uint32_t n,
                                                        SplConst k, uint32_t W, uint32_t H,
@@ -1633,7 +1635,7 @@ __global__ __launch_bounds__(256) void spl_rect_kernel(const float4 *__restrict_
     const double a = sqrt((c[0] - k.o[0]) * (c[0] - k.o[0]) + (c[1] - k.o[1]) * (c[1] - k.o[1]) +
                           (c[2] - k.o[2]) * (c[2] - k.o[2]));
     const double R = r + 2 * 3e-3 * (a + r) * 1.01 + 2 * k.e_abs;
-    int4 rect = make_int4(1, 0, 1, 0);  // empty
+    int4 rect = spl_empty();
     if (!isfinite(R) || !isfinite(a)) {
         atomicOr(flag, 1u);
         rects[i] = rect;
@@ -1687,7 +1689,7 @@ __global__ __launch_bounds__(256) void spl_fill_kernel(const int4 *__restrict__ 
     uint32_t cnt = flag[0] != 0u ? kSphListMaxDev + 1u : 0u, w0 = 0, w1 = 0;
     for (uint32_t b0 = 0; b0 < n; b0 += 256) {
         const uint32_t i = b0 + tid;
-        int4 r = make_int4(1, 0, 1, 0);
+        int4 r = spl_empty();
         if (i < n) r = rects[i];
         const bool keep = r.x <= tc1 && r.y >= tc0 && r.z <= tr1 && r.w >= tr0;
         const uint64_t m = __ballot(keep);
