@@ -15,7 +15,8 @@ import subprocess
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "lib", "libraytracer.so")
+# RT_AMD_LIB: another build of the library (A/B timing of build variants)
+LIB_PATH = os.environ.get("RT_AMD_LIB") or os.path.join(HERE, "lib", "libraytracer.so")
 
 RNG_COUNTER, RNG_REPLAY, RNG_SERIAL = 1, 2, 3
 ACCEL_AUTO, ACCEL_BRUTE, ACCEL_BVH = 0, 1, 2
