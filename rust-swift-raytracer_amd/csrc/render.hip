@@ -517,7 +517,7 @@ __device__ __forceinline__ bool tri_node(const TraceParams &p, F3 nlo, F3 nhi, F
     // NaN tn only comes from a NaN ray, which records no triangle)
     const bool skip = tn > tf || tf < 0.001f || __float_as_int(tn) > __float_as_int(cap);
     // a: child | axis << 29, or leaf bit | first << 3 | count; in a leaf-link
-    // image (static tree, runtime.cpp leaf_link_image) every node here is
+    // image (static tree, bvh.cpp leaf_link_image) every node here is
     // interior and a is the child link itself (kLeafBit | record for a leaf)
     const bool links = !cam && p.tleaf_links != 0;
     const bool is_leaf = !links && (a & kLeafBitDev) != 0;
