@@ -836,42 +836,4 @@ PrimaryTriLists build_primary_tri_lists(const CameraTriangleBVH &ct, const Camer
     return out;
 }
 
-// Leaf-link image of the static triangle tree (leaf size 1 only): every link
-// to a leaf node (an interior node's child word, any node's DFS link) becomes
-// kLeafBit | record, and the record's (v1).w holds the leaf's own link.  The
-// walk then goes from an interior node straight to the triangle's record: one
-// 64-B record load replaces the leaf's node load, its box test and the
-// dependent plane-then-edges record loads.  Dropping the leaf's box test only
-// adds triangle tests, and Mesh::hit's (t, index) argmin does not depend on
-// which extra triangles are tested (order independence).
-// Interior child words lose their axis bits (the kernel never reads them).
-// Returns false (image untouched) when a leaf holds more than one triangle,
-// the root is a leaf or a record index needs the leaf bit.
-bool leaf_link_image(std::vector<uint32_t> &q, std::vector<float> &tris) {
-    const size_t n = q.size() / 8;
-    if (n == 0 || (q[6] & kLeafBit) || tris.size() / 16 >= (size_t)kLeafBit) return false;
-    for (size_t i = 0; i < n; ++i) {
-        const uint32_t a = q[i * 8 + 6];
-        if ((a & kLeafBit) && (a & 7u) != 1u) return false;
-    }
-    auto relink = [&](uint32_t l) -> uint32_t {
-        if (l == kNodeEnd) return l;
-        const uint32_t a = q[(size_t)l * 8 + 6];
-        return (a & kLeafBit) ? kLeafBit | ((a & ~kLeafBit) >> 3) : l;
-    };
-    std::vector<uint32_t> out = q;
-    for (size_t i = 0; i < n; ++i) {
-        const uint32_t a = q[i * 8 + 6];
-        out[i * 8 + 7] = relink(q[i * 8 + 7]);
-        if (a & kLeafBit) {
-            const uint32_t rec = (a & ~kLeafBit) >> 3, link = relink(q[i * 8 + 7]);
-            std::memcpy(&tris[(size_t)rec * 16 + 11], &link, 4);
-        } else {
-            out[i * 8 + 6] = relink(a & 0x1FFFFFFFu);
-        }
-    }
-    q.swap(out);
-    return true;
-}
-
 }  // namespace rtamd

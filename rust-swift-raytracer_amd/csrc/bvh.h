@@ -102,11 +102,6 @@ struct CameraTriangleBVH {
 };
 // tree = false: the records and rec_box only (triangle order, no nodes), all
 // the primary strip lists need; bounce-0 rays then never walk this tree.
-// Rewrites a static tree's kernel image (qnodes, tris) so links to
-// single-triangle leaves point at the record (kLeafBit | record) and each
-// record's (v1).w holds its leaf's link (bvh.cpp; false: image untouched).
-bool leaf_link_image(std::vector<uint32_t> &qnodes, std::vector<float> &tris);
-
 CameraTriangleBVH build_camera_triangle_bvh(const std::vector<Triangle> &tris,
                                             const std::vector<float> &tri_hot, const TriangleBVH &tb,
                                             const float origin[3], uint32_t leaf_size, bool tree = true);

@@ -85,7 +85,6 @@ struct TraceParams {
     const float4 *tbvh_tris;  // 4 per triangle in tree order: (n, n.v0) (v0, id) (v1) (v2)
     const uint32_t *tbvh_loose;  // triangles tested by brute force, ascending
     uint32_t tnodes, ttris, tloose;
-    uint32_t tleaf_links;     // static tree as a leaf-link image (bvh.cpp leaf_link_image)
     float tbvh_c[3], tbvh_r, tbvh_mag;
     float tbvh_oc[3];         // origin the boxes were built for (widening uses o - oc)
     float tq_base[3], tq_step[3], tq_nbase, tq_nstep;  // static-tree grids

@@ -386,20 +386,11 @@ __device__ __forceinline__ bool tri_merge(float t, int idx, float &tri_t, int &t
 // One tree-ordered triangle record (bvh.h TriangleBVH::tris).
 __device__ __forceinline__ bool tri_record(const float4 *r, F3 org, F3 dir, float best_t,
                                            float &tri_t, int &tri_i, uint32_t &tri_in) {
-#if RT_TRI_REC_ONE
-    // the whole 64-B record in one round trip (the edges are loaded before
-    // the plane test is known)
-    const float4 N = r[0], A = r[1], B = r[2], Cc = r[3];
-    float t;
-    if (!tri_plane(N, org, dir, best_t, t)) return false;
-    ++tri_in;
-#else
     const float4 N = r[0];
     float t;
     if (!tri_plane(N, org, dir, best_t, t)) return false;
     ++tri_in;
     const float4 A = r[1], B = r[2], Cc = r[3];
-#endif
     if (!tri_edges(f3(N.x, N.y, N.z), f3(A.x, A.y, A.z), f3(B.x, B.y, B.z), f3(Cc.x, Cc.y, Cc.z),
                    org + scale(dir, t)))
         return false;
@@ -516,12 +507,9 @@ __device__ __forceinline__ bool tri_node(const TraceParams &p, F3 nlo, F3 nhi, F
     // tn > cap as an integer compare (cap > 0 or +inf; see sphere_node: a
     // NaN tn only comes from a NaN ray, which records no triangle)
     const bool skip = tn > tf || tf < 0.001f || __float_as_int(tn) > __float_as_int(cap);
-    // a: child | axis << 29, or leaf bit | first << 3 | count; in a leaf-link
-    // image (static tree, bvh.cpp leaf_link_image) every node here is
-    // interior and a is the child link itself (kLeafBit | record for a leaf)
-    const bool links = !cam && p.tleaf_links != 0;
-    const bool is_leaf = !links && (a & kLeafBitDev) != 0;
-    const uint32_t child = links ? a : a & 0x1FFFFFFFu;
+    // a: child | axis << 29, or leaf bit | first << 3 | count
+    const bool is_leaf = (a & kLeafBitDev) != 0;
+    const uint32_t child = a & 0x1FFFFFFFu;
     node = (skip || is_leaf) ? miss : child;
     leaf = a & ~kLeafBitDev;  // read only when the flag is set
     return !skip && is_leaf;
@@ -976,26 +964,9 @@ void trace_kernel(TraceParams p) {
                 F3 nlo, nhi;
                 sphere_slabs(org, inv, e, nlo, nhi);
                 float cap = fminf(best_t, tri_t);
-                const bool links = !cam && p.tleaf_links != 0;
                 do {
                     uint32_t leaf;
-                    if (links && (node & kLeafBitDev)) {
-                        // a leaf link: the record itself, its (v1).w the next link
-                        // (the whole 64-B record in one round trip: the link
-                        // needs (v1) anyway)
-                        const float4 *r = p.tbvh_tris + 4u * (node & ~kLeafBitDev);
-                        const float4 N = r[0], A = r[1], B = r[2], Cc = r[3];
-                        node = __float_as_uint(B.w);
-                        ++tri_done;
-                        float t;
-                        if (tri_plane(N, org, dir, best_t, t)) {
-                            ++tri_in;
-                            if (tri_edges(f3(N.x, N.y, N.z), f3(A.x, A.y, A.z), f3(B.x, B.y, B.z),
-                                          f3(Cc.x, Cc.y, Cc.z), org + scale(dir, t)) &&
-                                tri_merge(t, (int)__float_as_uint(A.w), tri_t, tri_i))
-                                cap = fminf(best_t, tri_t);
-                        }
-                    } else if (tri_node(p, nlo, nhi, inv, dlt2, cam, cap, node, leaf, tnode_tests)) {
+                    if (tri_node(p, nlo, nhi, inv, dlt2, cam, cap, node, leaf, tnode_tests)) {
                         tri_leaf(p, org, dir, cam, leaf, best_t, tri_t, tri_i, tri_in, tri_done);
                         cap = fminf(best_t, tri_t);
                     }

@@ -178,11 +178,8 @@ static int device_for(WorldState &w, int want, DeviceState *&out) {
                 if (e != hipSuccess || src.empty()) return e;
                 return hipMemcpy(*dst, src.data(), src.size() * sizeof(uint32_t), hipMemcpyHostToDevice);
             };
-            std::vector<uint32_t> qn = tb.qnodes;
-            std::vector<float> tr = tb.tris;
-            d->tleaf_links = env_u64("RT_AMD_TRI_LEAF_LINKS", 0) != 0 && leaf_link_image(qn, tr);
-            HIP_TRY(upu((void **)&d->tbvh_nodes, qn));
-            HIP_TRY(up((void **)&d->tbvh_tris, tr));
+            HIP_TRY(upu((void **)&d->tbvh_nodes, tb.qnodes));
+            HIP_TRY(up((void **)&d->tbvh_tris, tb.tris));
             HIP_TRY(upu((void **)&d->tbvh_loose, tb.loose));
             d->tnodes = (uint32_t)(tb.qnodes.size() / 8);
             d->ttris = (uint32_t)(tb.tris.size() / 16);
@@ -526,7 +523,6 @@ int render_frame(WorldState &w, const CameraModel &cam, size_t width, size_t hei
         p.tbvh_nodes = d->tbvh_nodes;
         p.tbvh_tris = d->tbvh_tris; p.tbvh_loose = d->tbvh_loose;
         p.tnodes = d->tnodes; p.ttris = d->ttris; p.tloose = d->tloose;
-        p.tleaf_links = d->tleaf_links;
         for (int k = 0; k < 3; ++k) {
             p.tbvh_c[k] = tb.centre[k];
             p.tbvh_oc[k] = tb.oc[k];

@@ -42,7 +42,6 @@ struct DeviceState {
     float4 *tbvh_tris = nullptr;
     uint32_t *tbvh_loose = nullptr;
     uint32_t tnodes = 0, ttris = 0, tloose = 0;
-    uint32_t tleaf_links = 0;                                   // leaf_link_image applied
     uint4 *cam_nodes = nullptr;                                 // camera-origin triangle BVH
     float4 *cam_tris = nullptr;
     uint32_t cam_nnodes = 0;

@@ -134,35 +134,6 @@ int main(int argc, char **argv) {
         check_quant(cb.nodes, 8, cb.qnodes, cb.miss, cb.qbox, 0, 1, "camera");
         CHECK(cb.tris.size() == tb.tris.size(), "camera tree holds %zu records, static %zu\n",
               cb.tris.size() / 16, tb.tris.size() / 16);
-        // leaf-link image (leaf size 1 only): a walk that enters every
-        // interior node reaches every record exactly once and then the end;
-        // a walk that skips the root ends at once
-        std::vector<uint32_t> q = tb.qnodes;
-        std::vector<float> r = tb.tris;
-        const bool linked = leaf_link_image(q, r);
-        CHECK(!linked || leaf == 1, "leaf-link image applied with leaf size %u\n", leaf);
-        if (linked) std::printf("leaf links\n");
-        if (linked) {
-            const size_t nrec = r.size() / 16;
-            std::vector<int> seen(nrec, 0);
-            uint32_t node = 0;
-            size_t steps = 0;
-            while (node != kNodeEnd && steps++ < 4 * q.size()) {
-                if (node & kLeafBit) {
-                    const uint32_t rec = node & ~kLeafBit;
-                    if (rec >= nrec) { CHECK(false, "record link %u out of range\n", rec); break; }
-                    seen[rec]++;
-                    node = bits(r[(size_t)rec * 16 + 11]);
-                } else {
-                    CHECK(!(tb.qnodes[(size_t)node * 8 + 6] & kLeafBit), "walk entered leaf node %u\n", node);
-                    node = q[(size_t)node * 8 + 6];
-                }
-            }
-            for (size_t j = 0; j < nrec; ++j) CHECK(seen[j] == 1, "record %zu reached %d times\n", j, seen[j]);
-            CHECK(q[7] == kNodeEnd, "root link %u\n", q[7]);
-            for (size_t j = 0; j < r.size(); ++j)
-                if (j % 16 != 11) CHECK(bits(r[j]) == bits(tb.tris[j]), "record word %zu changed\n", j);
-        }
     }
     // every triangle is in the tree, brute-forced (loose) or degenerate (n = 0)
     size_t in_tree = tb.tris.size() / 16, degenerate = 0;

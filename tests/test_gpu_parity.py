@@ -505,34 +505,6 @@ def test_triangle_bvh_c5_equals_brute_force():
     assert sa["rays"] == sb["rays"]
 
 
-@pytest.mark.parametrize("links", ["0", "1"])
-@pytest.mark.parametrize("case", [
-    dict(seed=12, n=400, size=2.0, dup=80, slivers=30),
-    dict(seed=15, n=400, offset=(2500.0, -1800.0, 900.0), cam=(2500.0, -1800.0, 900.0)),
-    dict(seed=17, n=200, grid=20, cam=(0.0, 6.0, -4.0)),
-    "c5",
-])
-def test_triangle_leaf_links_equal_brute_force(monkeypatch, case, links):
-    """The static tree walked as a leaf-link image (links to single-triangle
-    leaves go straight to the record, runtime.cpp leaf_link_image) and as the
-    plain node image: every sample equals brute force either way; a tree with
-    larger leaves keeps the plain image."""
-    monkeypatch.setenv("RT_AMD_TRI_LEAF_LINKS", links)
-    if case == "c5":
-        src, (w, h, spp) = S.mesh(), (480, 270, 2)
-    else:
-        src, (w, h, spp) = _triangle_scene(**case), (96, 64, 8)
-    a, sa, sma, b, sb, smb = _both_modes(src, w, h, spp)
-    assert sb["tri_bvh"] == 1
-    assert_bits_equal(b, a, "frame")
-    assert np.array_equal(smb[:, :3].view(np.uint32), sma[:, :3].view(np.uint32))
-    assert sa["rays"] == sb["rays"]
-    if case != "c5":
-        monkeypatch.setenv("RT_AMD_TRI_LEAF", "2")  # leaves of 2: plain image
-        c, _ = render_kept(R.World(src), w, h, spp, 8, accel=R.ACCEL_BVH)
-        assert_bits_equal(c, a, "frame, leaf size 2")
-
-
 @pytest.mark.parametrize("lists", ["1", "0"])
 def test_triangle_camera_tree_follows_camera_moves(monkeypatch, lists):
     """Bounce-0 rays use the phantom records of the camera origin -- through
