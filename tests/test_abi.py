@@ -150,3 +150,18 @@ def test_write_ppm(tmp_path):
     p = tmp_path / "x.ppm"
     R.write_ppm(img, str(p))
     assert p.read_text() == O.ppm(img).decode()
+
+
+def test_render_null_arguments_return_empty_framebuffer():
+    """A caller's bad arguments (NULL handle, NULL pixels) come back as the
+    documented {0, 0, NULL} framebuffer, with or without a GPU, and a NULL
+    camera is passed through by move_camera_position (lib.rs:49-63)."""
+    px = np.zeros((8, 8, 4), np.uint8)
+    fb = R.CFramebuffer(8, 8, px.ctypes.data_as(C.POINTER(R.ColorU8)))
+    res = R.lib().render(fb, None)
+    assert not res.pixels and res.width == 0 and res.height == 0
+    w = R.World(scene_text("world.txt"))
+    res = R.lib().render(R.CFramebuffer(8, 8, None), w.handle)
+    assert not res.pixels and res.width == 0 and res.height == 0
+    assert not px.any()
+    assert not R.lib().move_camera_position(None, 0.0, 0.0, 1.0)
