@@ -18,7 +18,10 @@ enum : uint32_t { kRngCounter = 1, kRngReplay = 2 };
 enum : uint32_t { kRngSerialCount = 3, kRngSerialEstimate = 4 };
 enum : uint32_t { kMatDiffuse = 0, kMatMetal = 1, kMatDielectric = 2, kMatEmission = 3 };
 constexpr uint32_t kPrimaryTriStripW = 8;  // bvh.h kTriStripW
-constexpr uint32_t kTraceRing = 4;         // chunk slots per wave (fused resolve)
+#ifndef RT_TRACE_RING
+#define RT_TRACE_RING 4
+#endif
+constexpr uint32_t kTraceRing = RT_TRACE_RING;  // chunk slots per wave (fused resolve)
 constexpr uint32_t kStatSlots = 16;        // u64 counters per wave record (TraceParams::stats)
 
 // Kernel argument block (lives in the kernarg segment -> SGPRs).

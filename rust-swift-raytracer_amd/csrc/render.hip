@@ -808,6 +808,13 @@ void trace_kernel(TraceParams p) {
         return b + (sl & ((1u << p.ring_shift) - 1u));
     };
 
+#ifdef RT_WAVE_TIMES
+    // diagnostic build only: per-wave timeline on the 100 MHz constant clock
+    // (start, last chunk pulled, queue found empty, exit; tools/tail_probe.py)
+    const uint64_t wt_start = __builtin_amdgcn_s_memrealtime();
+    uint64_t wt_pull = wt_start, wt_exh = wt_start;
+    uint32_t wt_jobs_tail = 0;  // jobs claimed in the wave's last chunk
+#endif
 #ifdef RT_STAMPS
     // diagnostic build only: wave cycles per loop segment (s_memtime deltas)
     uint64_t stamp_acc[4] = {0, 0, 0, 0};
@@ -1135,9 +1142,16 @@ void trace_kernel(TraceParams p) {
                 pend = __builtin_amdgcn_readfirstlane(pend);
                 if (base >= pend) {
                     exhausted = true;
+#ifdef RT_WAVE_TIMES
+                    wt_exh = __builtin_amdgcn_s_memrealtime();
+#endif
                 } else {
                     pool_next = base;
                     pool_end = min(base + p.chunk, pend);
+#ifdef RT_WAVE_TIMES
+                    wt_pull = __builtin_amdgcn_s_memrealtime();
+                    wt_jobs_tail = pool_end - pool_next;
+#endif
                     if (fused) {
                         const uint32_t k = (uint32_t)__builtin_ctz(rfree);
                         rfree &= ~(1u << k);
@@ -1234,6 +1248,13 @@ void trace_kernel(TraceParams p) {
         for (int k = 0; k < 4; ++k) w[10 + k] += mix[k];
 #ifdef RT_STAMPS
         for (int k = 0; k < 4; ++k) w[4 + k] += stamp_acc[k];
+#endif
+#ifdef RT_WAVE_TIMES
+        w[4] = wt_start;
+        w[5] = wt_pull;
+        w[6] = wt_exh;
+        w[7] = __builtin_amdgcn_s_memrealtime();
+        w[14] = wt_jobs_tail;
 #endif
     }
 }

@@ -690,6 +690,12 @@ int render_frame(WorldState &w, const CameraModel &cam, size_t width, size_t hei
     std::vector<unsigned long long> rec(max_waves * kStatSlots);
     HIP_TRY(hipMemcpyAsync(rec.data(), d->stats, rec.size() * 8, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
+    if (const char *dump = std::getenv("RT_AMD_WAVE_DUMP")) {  // diagnostic: raw per-wave records
+        if (FILE *f = std::fopen(dump, "wb")) {
+            std::fwrite(rec.data(), 8, rec.size(), f);
+            std::fclose(f);
+        }
+    }
     unsigned long long st[kStatSlots] = {};
     for (size_t i = 0; i < rec.size(); ++i) st[i % kStatSlots] += rec[i];
     if (stats) {
