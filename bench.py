@@ -130,6 +130,8 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--accel", default="auto", choices=["auto", "brute", "bvh"])
+    ap.add_argument("--no-serial", action="store_true",
+                    help="skip the RT_RNG_SERIAL (reference-identical render()) legs")
     args = ap.parse_args()
     launched = "WORLD_SIZE" in os.environ  # torchrun: one process per GPU
     world_size = int(os.environ.get("WORLD_SIZE", "1"))
@@ -209,6 +211,64 @@ def _post_move(world, step, sync, dz=-0.05):
             "steady_lists": int(st["primary_lists"] or st["camera_tree"])}
 
 
+SERIAL_CASES = (
+    # (label, scene, width, height, spp, depth): render()'s defaults (lib.rs:51)
+    # on the Swift app's world.txt at GameView-like window sizes, and the
+    # BASELINE C2 settings on the RTOW scene
+    ("world.txt 960x540 render()", "world", 960, 540, 16, 8),
+    ("world.txt 1920x1080 render()", "world", 1920, 1080, 16, 8),
+    ("c2 settings (rtow 1920x1080x64/8)", "rtow", 1920, 1080, 64, 8),
+)
+
+
+def serial_legs(reps=2):
+    """The reference-identical mode (RT_RNG_SERIAL, render()'s default: the
+    one xorshift32 stream of common.rs:321, resolved on the GPU and rendered
+    bit for bit): wall time per frame through the C-ABI, start-state search
+    time, iterations, and the frame right after move_camera_position
+    (GameView.swift:198-219) against steady frames.  Every frame's chain is
+    checked once (RT_FLAG_SERIAL_CHECK) outside the timed calls."""
+    out = []
+    for label, scene, W, H, spp, depth in SERIAL_CASES:
+        src = S.read("world.txt") if scene == "world" else S.rtow()
+        world = R.World(src)
+        _, chk = world.render(W, H, spp, depth, mode=R.RNG_SERIAL, serial_check=True)
+        times, st = [], None
+        for _ in range(reps):
+            t = time.perf_counter()
+            if (spp, depth) == (16, 8):
+                world.render_reference(W, H)  # render() itself: host frame, synchronous
+            else:
+                world.render(W, H, spp, depth, mode=R.RNG_SERIAL, stats=False)
+            times.append(time.perf_counter() - t)
+        _, st = world.render(W, H, spp, depth, mode=R.RNG_SERIAL)
+        wall = min(times)
+        leg = {"case": label, "width": W, "height": H, "spp": spp, "depth": depth,
+               "samples": W * H * spp, "ms_per_frame": wall * 1e3,
+               "mrays_per_s": st["rays"] / wall / 1e6, "msamples_per_s": W * H * spp / wall / 1e6,
+               "start_states_ms": st["serial_ms"], "tables_ms": st["serial_setup_ms"],
+               "replay_trace_ms": st["trace_ms"], "iterations": st["serial_iterations"],
+               "iterations_stopped_short": st["serial_retries"],
+               "chain_checked": chk["serial_checked"], "chain_breaks": chk["serial_chain_breaks"],
+               "api": "render()" if (spp, depth) == (16, 8) else "rt_render_ex SERIAL"}
+        if scene == "world" and W == 960:
+            world.move_camera(0.0, 0.0, -0.05)
+            t = time.perf_counter()
+            world.render_reference(W, H)
+            first = time.perf_counter() - t
+            steady = []
+            for _ in range(reps):
+                t = time.perf_counter()
+                world.render_reference(W, H)
+                steady.append(time.perf_counter() - t)
+            leg["post_move"] = {"move": [0.0, 0.0, -0.05], "first_frame_ms": first * 1e3,
+                                "steady_frame_ms": min(steady) * 1e3,
+                                "ratio": first / min(steady)}
+        out.append(leg)
+        world.close()
+    return out
+
+
 def single_process(args):
     """N GPUs from this one process through the library's multi-device mode
     (RtRenderOptions.ndevices): every device renders its row blocks, an RCCL
@@ -246,9 +306,12 @@ def single_process(args):
     rows = R.tile_rows(H, ROW_BLOCK, 0, ngpu) if ngpu > 1 else H
     par = (f"row-tiles x{ngpu} (block {ROW_BLOCK}), one process, RCCL ncclGather "
            f"({ranks} ranks) to device 0")
+    extra = {"rccl_ranks": ranks, "launch": "single process", "post_move": moved}
+    if ngpu == 1 and not args.no_serial:
+        torch.cuda.set_stream(torch.cuda.default_stream(dev))
+        extra["serial"] = serial_legs()
     _report(args, src, world, W, H, spp, depth, st0, st_warm["rays"] * args.steps, elapsed,
-            trace_ms, count_trace_ms, ngpu, rows, par,
-            {"rccl_ranks": ranks, "launch": "single process", "post_move": moved})
+            trace_ms, count_trace_ms, ngpu, rows, par, extra)
 
 
 def multi_process(args, world_size):

@@ -61,6 +61,15 @@ typedef struct RtRenderOptions {
  * rt_read_samples can then read.  Both give bit-identical frames. */
 enum { RT_FLAG_KEEP_SAMPLES = 1 };
 
+/* RT_RNG_SERIAL self-check.  RT_FLAG_SERIAL_CHECK traces every sample once
+ * more from the start state found for it and checks the chain the reference's
+ * one stream forms (common.rs:321-341): sample 0 starts at the seed, and each
+ * sample's end state is the next sample's start state (the last one's: the
+ * stream state the search ended on).  Mismatches are counted in
+ * RtRenderStats.serial_chain_breaks (0 = the start states are the
+ * reference's). */
+enum { RT_FLAG_SERIAL_CHECK = 2 };
+
 /* Sphere search.  Both give bit-identical frames:
  *   RT_ACCEL_BRUTE: every sphere in file order (common.rs:241-247).
  *   RT_ACCEL_BVH:   exact-pruning BVHs: spheres (BRUTE below 16 spheres) and
@@ -98,6 +107,13 @@ typedef struct RtRenderStats {
                                 candidate lists (0 right after a camera move or
                                 resize while they are built on a host thread) */
   uint32_t camera_tree;      /* 1: bounce-0 triangle rays used the camera-origin records (tree or strip lists) */
+  uint32_t serial_iterations;   /* RT_RNG_SERIAL: candidate-table iterations run   */
+  uint64_t serial_checked;      /* RT_FLAG_SERIAL_CHECK: samples whose chain link
+                                   was checked (0 without the flag)             */
+  uint64_t serial_chain_breaks; /* RT_FLAG_SERIAL_CHECK: broken links (0 = the
+                                   reference's stream)                          */
+  double serial_setup_ms;       /* RT_RNG_SERIAL: HIP-event time of the estimate
+                                   pass and its tables (part of serial_ms)      */
 } RtRenderStats;
 
 /* spp 16, depth 8 (lib.rs:51), SERIAL, seed 2547549, one rank, device -1,
@@ -105,8 +121,9 @@ typedef struct RtRenderStats {
  * environment variables: RT_AMD_RNG=counter selects RT_RNG_COUNTER (fast,
  * statistically equal frames) instead of the reference's stream, and
  * RT_AMD_DEVICES=N (N >= 1) row-tiles its frames over N GPUs (in SERIAL mode
- * every device finds the whole frame's start states itself: the stream is one
- * sequential dependency, so only the REPLAY render is split). */
+ * the first device finds the whole frame's start states -- the stream is one
+ * sequential dependency -- and broadcasts them over RCCL; the REPLAY render is
+ * split). */
 void rt_default_options(RtRenderOptions *opts);
 
 /* Rows of a `height`-row image that belong to `rank` (see RtRenderOptions). */
@@ -135,8 +152,11 @@ int rt_render_ex(Rust_CFramebuffer framebuffer, const Rust_WorldHandle *handle,
  * stays resident on the device between calls.  With `stats`, returns after the
  * frame is complete (HIP-event timings and counters filled in); with
  * stats == NULL the frame is only enqueued on the stream (no host wait), so
- * consecutive frames and the caller's collectives pipeline.  Returns 0 or a
- * negative error. */
+ * consecutive frames and the caller's collectives pipeline -- except in
+ * RT_RNG_SERIAL mode, whose start-state search reads its progress back and
+ * waits on the host between batches of iterations (the REPLAY render that
+ * follows is only enqueued); do not call it inside a stream capture.  Returns
+ * 0 or a negative error. */
 int rt_render_device(const Rust_WorldHandle *handle, size_t width, size_t height,
                      const RtRenderOptions *opts, void *d_rgba, void *hip_stream,
                      RtRenderStats *stats);
@@ -177,6 +197,16 @@ int rt_last_parse_error(void);
 
 /* image.rs:59-81: writes an ASCII PPM (P3).  Returns 0 on success. */
 int rt_write_ppm(const Rust_CFramebuffer *framebuffer, const char *path);
+
+/* The last step of a multi-device frame (ndevices > 1), on its own: reads
+ * `nranks` tiles of `max_rows` rows each from DEVICE memory d_gathered (rank
+ * g's tile at row g*max_rows, tile row k = image row rt_tile_row(k), the
+ * layout the RCCL gather leaves on the first device) and writes the
+ * width x height frame to DEVICE memory d_out, on hip_stream (NULL: the null
+ * stream), without waiting.  Lets one GPU check the assembly for any rank
+ * count.  Returns 0 or a negative error. */
+int rt_assemble_tiles(const void *d_gathered, void *d_out, size_t width, size_t height, uint32_t row_block,
+                      uint32_t nranks, size_t max_rows, void *hip_stream);
 
 /* Number of HIP devices visible (0 if the runtime is unavailable). */
 int rt_device_count(void);

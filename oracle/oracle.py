@@ -64,6 +64,10 @@ def lib():
         L.ro_render.argtypes = [C.c_void_p, C.c_size_t, C.c_size_t, C.c_int, C.c_int, C.c_int,
                                 C.c_uint32, u32p, C.c_size_t, C.c_size_t, C.c_int,
                                 C.POINTER(C.c_uint8), u32p, fp, C.POINTER(Stats)]
+        L.ro_render_cols.restype = C.c_int
+        L.ro_render_cols.argtypes = [C.c_void_p, C.c_size_t, C.c_size_t, C.c_int, C.c_int, C.c_int,
+                                     C.c_uint32, u32p, C.c_size_t, C.c_size_t, C.c_size_t, C.c_size_t,
+                                     C.c_int, C.POINTER(C.c_uint8), u32p, fp, C.POINTER(Stats)]
         L.ro_xorshift32.restype = C.c_uint32
         L.ro_xorshift32.argtypes = [u32p]
         L.ro_random_f32.restype = C.c_float
@@ -150,7 +154,7 @@ class Scene:
 
     def render(self, width, height, spp, depth, mode=RNG_SERIAL, seed=DEFAULT_SEED,
                replay=None, row_begin=0, row_step=1, nthreads=1, record_states=False,
-               record_samples=False, out=None):
+               record_samples=False, out=None, col_begin=0, col_step=1):
         """Returns (rgba[H, W, 4] uint8, stats dict, states or None[, samples]).
 
         samples (when record_samples): float32[W*H*spp, 4] ray_color results
@@ -172,9 +176,9 @@ class Scene:
             samples = np.zeros((width * height * max(spp, 0), 4), np.float32)
             smp = fptr(samples)
         st = Stats()
-        rc = lib().ro_render(self._h, width, height, spp, depth, mode, seed, rp, row_begin,
-                             row_step, nthreads, out.ctypes.data_as(C.POINTER(C.c_uint8)), sp,
-                             smp, C.byref(st))
+        rc = lib().ro_render_cols(self._h, width, height, spp, depth, mode, seed, rp, row_begin,
+                                  row_step, col_begin, col_step, nthreads,
+                                  out.ctypes.data_as(C.POINTER(C.c_uint8)), sp, smp, C.byref(st))
         if rc != 0:
             raise RuntimeError(f"ro_render failed: {rc}")
         if record_samples:

@@ -667,16 +667,18 @@ uint32_t ro_sample_seed(uint32_t base_seed, uint64_t job) {
 // ray_trace, common.rs:320-361, generalised (see header).
 static void trace_rows(const ro_scene *sc, size_t W, size_t H, int spp, int depth, int mode,
                        uint32_t seed, const uint32_t *replay, size_t row_begin, size_t row_step,
-                       size_t thread, size_t nthreads, uint8_t *out, uint32_t *states,
-                       float *sample_rgba, Counters &cnt, uint64_t &samples) {
+                       size_t col_begin, size_t col_step, size_t thread, size_t nthreads, uint8_t *out,
+                       uint32_t *states, float *sample_rgba, Counters &cnt, uint64_t &samples) {
     Rng rng{seed ? seed : kDefaultSeed};
     const float wden = (float)(W - 1);  // (width-1) as f32
     const float hden = (float)(H - 1);
     const float inv_spp = 1.0f / (float)spp;
     size_t k = 0;
     for (size_t row = row_begin; row < H; row += row_step, ++k) {
-        if (k % nthreads != thread) continue;
-        for (size_t col = 0; col < W; ++col) {
+        for (size_t col = col_begin; col < W; col += col_step) {
+            // (pixels dealt cyclically over the threads: a single row still
+            // uses every thread; per-sample RNG modes only)
+            if ((k * W + col) % nthreads != thread) continue;
             C4 color = color3(0.0f, 0.0f, 0.0f);  // alpha starts at 1.0
             for (int s = 0; s < spp; ++s) {
                 uint64_t job = ((uint64_t)row * W + col) * (uint64_t)spp + (uint64_t)s;
@@ -709,7 +711,16 @@ int ro_render(const ro_scene *s, size_t width, size_t height, int spp, int depth
               uint32_t seed, const uint32_t *replay_states, size_t row_begin, size_t row_step,
               int nthreads, uint8_t *out_rgba, uint32_t *sample_states, float *sample_rgba,
               ro_stats *stats) {
-    if (!s || !out_rgba || row_step == 0) return -1;
+    return ro_render_cols(s, width, height, spp, depth, rng_mode, seed, replay_states, row_begin, row_step, 0,
+                          1, nthreads, out_rgba, sample_states, sample_rgba, stats);
+}
+
+int ro_render_cols(const ro_scene *s, size_t width, size_t height, int spp, int depth, int rng_mode,
+                   uint32_t seed, const uint32_t *replay_states, size_t row_begin, size_t row_step,
+                   size_t col_begin, size_t col_step, int nthreads, uint8_t *out_rgba,
+                   uint32_t *sample_states, float *sample_rgba, ro_stats *stats) {
+    if (!s || !out_rgba || row_step == 0 || col_step == 0) return -1;
+    if (rng_mode == RO_RNG_SERIAL && (col_begin != 0 || col_step != 1)) return -1;  // (one stream: whole rows)
     if (rng_mode == RO_RNG_REPLAY && !replay_states) return -1;
     if (rng_mode == RO_RNG_SERIAL) nthreads = 1;  // one frame-wide stream: inherently serial
     if (nthreads < 1) nthreads = 1;
@@ -717,13 +728,13 @@ int ro_render(const ro_scene *s, size_t width, size_t height, int spp, int depth
     std::vector<uint64_t> samples((size_t)nthreads, 0);
     if (nthreads == 1) {
         trace_rows(s, width, height, spp, depth, rng_mode, seed, replay_states, row_begin, row_step,
-                   0, 1, out_rgba, sample_states, sample_rgba, cnt[0], samples[0]);
+                   col_begin, col_step, 0, 1, out_rgba, sample_states, sample_rgba, cnt[0], samples[0]);
     } else {
         std::vector<std::thread> th;
         for (int t = 0; t < nthreads; ++t)
             th.emplace_back([&, t] {
                 trace_rows(s, width, height, spp, depth, rng_mode, seed, replay_states, row_begin,
-                           row_step, (size_t)t, (size_t)nthreads, out_rgba, sample_states,
+                           row_step, col_begin, col_step, (size_t)t, (size_t)nthreads, out_rgba, sample_states,
                            sample_rgba, cnt[(size_t)t], samples[(size_t)t]);
             });
         for (auto &x : th) x.join();

@@ -71,13 +71,21 @@ uint32_t ro_sample_seed(uint32_t base_seed, uint64_t job);
  * job = (row*width + col)*spp + s.  replay_states: REPLAY input, same index.
  * sample_rgba (optional, width*height*spp*4 f32): every sample's ray_color
  * result (r, g, b, a), same job index -- the bit-level parity surface.
- * nthreads > 1 is allowed for COUNTER/REPLAY (rows dealt cyclically).
+ * nthreads > 1 is allowed for COUNTER/REPLAY (pixels dealt cyclically).
  * Returns 0 on success. */
 int ro_render(const ro_scene *s, size_t width, size_t height, int spp, int depth,
               int rng_mode, uint32_t seed, const uint32_t *replay_states,
               size_t row_begin, size_t row_step, int nthreads,
               uint8_t *out_rgba, uint32_t *sample_states, float *sample_rgba,
               ro_stats *stats);
+
+/* Same, over the columns col_begin, col_begin+col_step, ... of those rows only
+ * (COUNTER / REPLAY; SERIAL needs whole rows). */
+int ro_render_cols(const ro_scene *s, size_t width, size_t height, int spp, int depth,
+                   int rng_mode, uint32_t seed, const uint32_t *replay_states,
+                   size_t row_begin, size_t row_step, size_t col_begin, size_t col_step,
+                   int nthreads, uint8_t *out_rgba, uint32_t *sample_states,
+                   float *sample_rgba, ro_stats *stats);
 
 /* ---- known-answer hooks on single functions (tests only) ---------------- */
 uint32_t ro_xorshift32(uint32_t *state);                      /* random.rs:22-30 */

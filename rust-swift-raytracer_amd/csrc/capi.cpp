@@ -31,6 +31,16 @@ RtRenderOptions reference_options() {
     return o;
 }
 
+// A leaf-size knob (RT_AMD_LEAF / RT_AMD_TRI_LEAF): a whole decimal number in
+// [1, 8], else the default (the BVH builders clamp it as well)
+uint32_t env_leaf(const char *name, uint32_t dflt) {
+    const char *e = std::getenv(name);
+    if (!e || !*e) return dflt;
+    char *end = nullptr;
+    const long n = std::strtol(e, &end, 10);
+    return (end && *end == '\0' && n >= 1 && n <= 8) ? (uint32_t)n : dflt;
+}
+
 // render()'s device count: RT_AMD_DEVICES=N (N >= 1) row-tiles its frames over
 // N devices; unset, invalid or 0 keeps one device
 int32_t env_devices() {
@@ -61,15 +71,12 @@ Rust_WorldHandle *load_world(const char *source) {
     world->state.packed = rtamd::pack_scene(world->state.scene, 8, 1);
     // spheres per BVH leaf (A/B with walk gating, C2 / C3: 3 -> 4.72 / 70.6 ms,
     // 2 -> 4.65 / 69.6, 1 -> 6.33 / 95.3 -- its tree no longer fits 64 KB of LDS)
-    const char *leaf = std::getenv("RT_AMD_LEAF");
-    world->state.bvh = rtamd::build_sphere_bvh(world->state.scene.spheres,
-                                               leaf ? (uint32_t)std::atoi(leaf) : 2u);
+    world->state.bvh = rtamd::build_sphere_bvh(world->state.scene.spheres, env_leaf("RT_AMD_LEAF", 2u));
     // triangles per BVH leaf (A/B on C5 at 96-node walk slices: 1 -> 222 ms,
     // 2 -> 240, 3 -> 293)
-    const char *tleaf = std::getenv("RT_AMD_TRI_LEAF");
     world->state.tbvh = rtamd::build_triangle_bvh(world->state.scene.triangles,
                                                   world->state.packed.tri_hot,
-                                                  tleaf ? (uint32_t)std::atoi(tleaf) : 1u);
+                                                  env_leaf("RT_AMD_TRI_LEAF", 1u));
     // bounce-0 triangle tree for the scene camera (rebuilt by the first render
     // after move_camera_position, which does not see the world)
     rtamd::prepare_camera(world->state, world->state.scene.camera);
@@ -262,6 +269,12 @@ int rt_write_ppm(const Rust_CFramebuffer *fb, const char *path) {
 }
 
 int rt_comm_count(int first, int n) { return rtamd::comm_count(first, n); }
+
+int rt_assemble_tiles(const void *d_gathered, void *d_out, size_t width, size_t height, uint32_t row_block,
+                      uint32_t nranks, size_t max_rows, void *hip_stream) {
+    return rtamd::assemble_tiles(static_cast<const uint32_t *>(d_gathered), static_cast<uint32_t *>(d_out), width,
+                                 height, row_block, nranks, max_rows, static_cast<hipStream_t>(hip_stream));
+}
 
 int rt_device_count(void) {
     int n = 0;

@@ -15,7 +15,10 @@ enum : uint32_t { kRngCounter = 1, kRngReplay = 2 };
 // count b (the reference draws 2 + 3b numbers per sample) instead of a colour.
 //   kRngSerialCount: variant k = candidate; start state win[2 jl + 3 (lo[jl] + k)]
 //   kRngSerialEstimate: variant r = repetition; start state counter_seed(seed, j * V + r)
-enum : uint32_t { kRngSerialCount = 3, kRngSerialEstimate = 4 };
+//   kRngSerialCheck: one variant; start state win[j] (the found start states),
+//     stores 1 when the sample's end state is not win[j + 1] (p.seed: the
+//     stream state after the frame's last sample), else 0
+enum : uint32_t { kRngSerialCount = 3, kRngSerialEstimate = 4, kRngSerialCheck = 5 };
 enum : uint32_t { kMatDiffuse = 0, kMatMetal = 1, kMatDielectric = 2, kMatEmission = 3 };
 constexpr uint32_t kPrimaryTriStripW = 8;  // bvh.h kTriStripW
 #ifndef RT_TRACE_RING
@@ -23,6 +26,21 @@ constexpr uint32_t kPrimaryTriStripW = 8;  // bvh.h kTriStripW
 #endif
 constexpr uint32_t kTraceRing = RT_TRACE_RING;  // chunk slots per wave (fused resolve)
 constexpr uint32_t kStatSlots = 16;        // u64 counters per wave record (TraceParams::stats)
+
+// SERIAL prediction, per pixel (built on the device from the estimate pass,
+// render.hip launch_serial_tables): P[q] = sum over pixels p < q of spp mu[p]
+// (npix + 1 doubles), mu[p] the pixel's mean scatter count per sample.  The
+// predicted scatter count of frame samples [0, j) is
+// M(j) = P[p] + (j - p spp) mu[p], p = j / spp (P[npix] for j = npix spp).
+struct SerialPred {
+    const double *P;
+    const double *mu;
+    uint32_t spp, npix;
+};
+RT_HOST_DEVICE inline double serial_M(const SerialPred &m, uint32_t j) {
+    const uint32_t p = j / m.spp;
+    return p < m.npix ? m.P[p] + (double)(j - p * m.spp) * m.mu[p] : m.P[m.npix];
+}
 
 // Kernel argument block (lives in the kernarg segment -> SGPRs).
 struct TraceParams {
@@ -111,7 +129,7 @@ struct TraceParams {
     // sample jl is frame sample cbase + jl (reference order, common.rs:327-336),
     // clamped to nserial - 1
     const uint32_t *win;      // kRngSerialCount: stream states from sample cbase's start on
-    const double *sM;         // kRngSerialCount: prefix sums of the predicted scatter counts
+    SerialPred sM;            // kRngSerialCount: the predicted scatter counts (per pixel)
     const uint32_t *ctrl;     // serial control block (kRngSerialCount: cbase = ctrl[4];
                               // ctrl[0] != 0, the frame is resolved: exit at once)
     uint32_t cbase;           // first frame sample of the launch
@@ -122,13 +140,13 @@ struct TraceParams {
 };
 
 // Candidate k of chunk sample jl (frame sample a + jl) means B = serial_lo + k
-// scatters since sample a: the predicted offset (prefix sums M of the
-// per-sample means) minus K / 2, clamped to the possible [0, depth * jl].
-// Host, count kernel and walk kernels use this one definition.
-RT_HOST_DEVICE inline uint32_t serial_lo(const double *M, uint32_t a, uint32_t jl, uint32_t K,
+// scatters since sample a: the predicted offset M(a + jl) - M(a) minus K / 2,
+// clamped to the possible [0, depth * jl].  Count kernel and walk kernels use
+// this one definition.
+RT_HOST_DEVICE inline uint32_t serial_lo(const SerialPred &M, uint32_t a, uint32_t jl, uint32_t K,
                                          uint32_t depth, uint32_t nserial) {
     const uint32_t j = a + jl < nserial ? a + jl : nserial;
-    double c = __builtin_floor(M[j] - M[a]) - (double)(K / 2u);
+    double c = __builtin_floor(serial_M(M, j) - serial_M(M, a)) - (double)(K / 2u);
     const double hi = (double)depth * (double)jl;
     c = c < 0.0 ? 0.0 : c;
     c = c > hi ? hi : c;
@@ -144,6 +162,29 @@ hipError_t launch_trace(const TraceParams &p, uint32_t blocks, hipStream_t strea
 hipError_t launch_sphere_lists(const float4 *prims, uint32_t n, const double *Mi, const double *o,
                                double e_abs, double wden, double hden, uint32_t width, uint32_t height,
                                int4 *rects, uint32_t *flag, uint2 *rec, hipStream_t stream);
+// SERIAL mode, the estimate reduction (render_frame_serial step 1), on the
+// device.  tab holds, for a frame of npix pixels (serial_tab_doubles(npix)):
+//   P   [0, npix]             prefix sums of spp mu (SerialPred::P)
+//   mu  [npix + 1, 2 npix]    per-pixel mean scatter count (SerialPred::mu)
+//   V   [2 npix + 1, 4 npix + 1]  prefix sums of spp var (npix + 1), then var (npix)
+//   ss  [4 npix + 2, 5 npix + 1]  per-pixel sum of squared deviations of b
+//   sum [5 npix + 2, + 8)     {sum of ss, dmax (double bits), V(n0), lost-count flag}
+// Moments: pixels [pix0, pix0 + n) of one estimate launch, whose scatter
+// counts are est[(p - pix0) spp R + s R + r] (R traces per sample); var is
+// scaled by `scale` (the means' estimation error).  Tables: the prefix sums
+// (a fixed-shape scan: deterministic), dmax = the largest M(a + L + L/4) -
+// M(a) over a = 0, L/4, 2 L/4, ... (the candidate window's reach) and V(n0).
+size_t serial_tab_doubles(uint32_t npix);
+// Counts the nonzero flags of a kRngSerialCheck pass (plane 0 of the slab)
+// into *count (atomics; *count is not reset).
+hipError_t launch_serial_check_count(const float *flags, uint32_t n, unsigned long long *count,
+                                     hipStream_t stream);
+hipError_t launch_serial_moments(const float *est, uint32_t pix0, uint32_t n, uint32_t spp, uint32_t R,
+                                 double scale, double *tab, uint32_t npix, hipStream_t stream);
+hipError_t launch_serial_tables(double *tab, double *scratch, uint32_t npix, uint32_t spp, uint32_t L,
+                                uint32_t n0, hipStream_t stream);
+// doubles of launch_serial_tables' scratch
+size_t serial_scan_scratch(uint32_t npix);
 // SERIAL mode.  ctrl (u32[8]): {resolved, state at sample a, sum of b (low
 // bits), iterations, a = first unresolved sample, candidates per sample of the
 // next iteration (0: the launch's K), iterations that stopped short, 0}.
@@ -165,7 +206,7 @@ uint32_t serial_walk_block(uint32_t L);
 // the walk sets the next iteration's candidates per sample in ctrl[5] (<= K):
 // 2 z (sqrt(V over its L samples) + sfloor sqrt(L)) + 2 depth + 2; the count
 // pass and the walks use ctrl[5] when it is set.
-hipError_t launch_serial_walk(uint32_t *ctrl, const float *table, const double *M, const double *V,
+hipError_t launch_serial_walk(uint32_t *ctrl, const float *table, SerialPred M, const double *V,
                               uint32_t npix, uint32_t spp, float z, float sfloor, const uint32_t *win,
                               uint32_t *states, uint32_t *bend, uint32_t *path, uint32_t *fin, uint32_t L,
                               uint32_t K, uint32_t depth, uint32_t nserial, hipStream_t stream);

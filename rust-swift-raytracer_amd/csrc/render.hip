@@ -559,6 +559,7 @@ __device__ __forceinline__ uint32_t serial_start(const TraceParams &p, uint32_t 
     if (p.mode == kRngSerialCount)
         return p.win[2u * jl + 3u * (serial_lo(p.sM, p.cbase, jl, p.spp, (p.max_draws - 2u) / 3u,
                                                p.nserial) + k)];
+    if (p.mode == kRngSerialCheck) return p.win[p.cbase + jl];
     return counter_seed(p.seed, (uint64_t)(p.cbase + jl) * p.spp + k);
 }
 
@@ -1063,7 +1064,12 @@ void trace_kernel(TraceParams p) {
             }
             RT_STAMP(3);
             if (done) {
-                if (kSerial) {
+                if (kSerial && p.mode == kRngSerialCheck) {
+                    // the chain check: this sample's end state must be the next
+                    // sample's start state (one variant: slot = launch sample)
+                    const uint32_t j = p.cbase + slot;
+                    out_r = rng == (j + 1u < p.nserial ? p.win[j + 1u] : p.seed) ? 0.0f : 1.0f;
+                } else if (kSerial) {
                     // SERIAL passes: the sample's scatter count b instead of its
                     // colour -- the draws it consumed (2 + 3b, common.rs:335-336 and
                     // random_unit_sphere per diffuse/metal scatter, common.rs:32-38)
@@ -1458,7 +1464,7 @@ __global__ __launch_bounds__(256) void serial_window_kernel(const uint32_t *__re
 //     start, writing start states (win[2 jl + 3 B]); ctrl advances past the
 //     resolved samples (>= 1: sample a's own window always holds B = 0).
 constexpr uint32_t kWalkInvalid = 0xFFFFFFFFu;
-__device__ __forceinline__ uint32_t walk_step(const float *table, const double *M, uint32_t a,
+__device__ __forceinline__ uint32_t walk_step(const float *table, const SerialPred &M, uint32_t a,
                                               uint32_t K, uint32_t depth, uint32_t nserial, uint32_t jl,
                                               uint32_t B) {
     const uint32_t l = serial_lo(M, a, jl, K, depth, nserial);
@@ -1476,7 +1482,7 @@ __device__ __forceinline__ uint32_t serial_k(const uint32_t *ctrl, uint32_t K) {
 // sample-major (path[(jl - j0) * nb * K + t], coalesced), so that the states
 // of the true path are a gather (serial_states_kernel), not a re-walk
 __global__ __launch_bounds__(256) void serial_walk_blocks_kernel(
-    const uint32_t *__restrict__ ctrl, const float *__restrict__ table, const double *__restrict__ M,
+    const uint32_t *__restrict__ ctrl, const float *__restrict__ table, SerialPred M,
     uint32_t *__restrict__ bend, uint32_t *__restrict__ path, uint32_t L, uint32_t K, uint32_t R,
     uint32_t depth, uint32_t nserial) {
     if (ctrl[0] != 0u) return;
@@ -1498,7 +1504,7 @@ __global__ __launch_bounds__(256) void serial_walk_blocks_kernel(
 }
 
 __global__ __launch_bounds__(256) void serial_walk_finish_kernel(
-    uint32_t *__restrict__ ctrl, const float *__restrict__ table, const double *__restrict__ M,
+    uint32_t *__restrict__ ctrl, const float *__restrict__ table, SerialPred M,
     const double *__restrict__ V, uint32_t npix, uint32_t spp, const uint32_t *__restrict__ win,
     const uint32_t *__restrict__ bend, uint32_t *__restrict__ states, uint32_t *__restrict__ fin, uint32_t L,
     uint32_t Kmax, uint32_t R, uint32_t depth, uint32_t nserial, float z, float sfloor) {
@@ -1601,6 +1607,209 @@ __global__ __launch_bounds__(256) void serial_states_kernel(const uint32_t *__re
     states[fin[0] + jl] = win[2u * jl + 3u * B];
 }
 
+// ---- the estimate reduction (render.h serial_tab_doubles for the layout)
+// One thread per pixel: its spp * R scatter counts (contiguous) summed in
+// double; a negative or NaN count (a lost draw count) raises the flag.
+__global__ __launch_bounds__(256) void serial_moments_kernel(const float *__restrict__ est, uint32_t pix0,
+                                                             uint32_t n, uint32_t spp, uint32_t R,
+                                                             double scale, double *__restrict__ tab,
+                                                             uint32_t npix) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t per = spp * R;
+    const float *src = est + (size_t)i * per;
+    double s = 0.0, sq = 0.0;
+    bool bad = false;
+    for (uint32_t k = 0; k < per; ++k) {
+        const float b = src[k];
+        bad |= !(b >= 0.0f);
+        s += (double)b;
+        sq += (double)b * (double)b;
+    }
+    const uint32_t p = pix0 + i;
+    const double mu = s / (double)per;
+    const double v = sq / (double)per - mu * mu;
+    tab[npix + 1 + p] = mu;
+    tab[3 * (size_t)npix + 2 + p] = (v > 0.0 ? v : 0.0) * scale;
+    tab[4 * (size_t)npix + 2 + p] = sq - s * mu;
+    if (bad) tab[5 * (size_t)npix + 5] = 1.0;
+}
+
+// Prefix sums over pixels of (spp mu, spp var, ss) in tiles of kScanTile:
+// tile totals, one workgroup's exclusive scan of the totals, then each tile's
+// own scan from its offset.  The shape is fixed, so the sums are the same
+// bits on every call.
+constexpr uint32_t kScanTile = 1024;
+__device__ __forceinline__ void scan_inputs(const double *tab, uint32_t npix, uint32_t spp, uint32_t p,
+                                            double v[3]) {
+    if (p >= npix) { v[0] = v[1] = v[2] = 0.0; return; }
+    v[0] = (double)spp * tab[npix + 1 + p];
+    v[1] = (double)spp * tab[3 * (size_t)npix + 2 + p];
+    v[2] = tab[4 * (size_t)npix + 2 + p];
+}
+
+// inclusive scan of 256 values x 3 across the workgroup (Hillis-Steele in LDS)
+__device__ __forceinline__ void block_scan3(double (*sh)[256], double v[3]) {
+    const uint32_t t = threadIdx.x;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) sh[c][t] = v[c];
+    __syncthreads();
+    for (uint32_t off = 1; off < 256; off <<= 1) {
+        double a[3];
+#pragma unroll
+        for (int c = 0; c < 3; ++c) a[c] = t >= off ? sh[c][t - off] : 0.0;
+        __syncthreads();
+#pragma unroll
+        for (int c = 0; c < 3; ++c) sh[c][t] += a[c];
+        __syncthreads();
+    }
+#pragma unroll
+    for (int c = 0; c < 3; ++c) v[c] = sh[c][t];
+    __syncthreads();
+}
+
+__global__ __launch_bounds__(256) void serial_scan_tiles_kernel(const double *__restrict__ tab, uint32_t npix,
+                                                                uint32_t spp, double *__restrict__ tsum) {
+    __shared__ double sh[3][256];
+    const uint32_t p0 = blockIdx.x * kScanTile + threadIdx.x * 4u;
+    double acc[3] = {0.0, 0.0, 0.0};
+    for (uint32_t k = 0; k < 4; ++k) {
+        double v[3];
+        scan_inputs(tab, npix, spp, p0 + k, v);
+#pragma unroll
+        for (int c = 0; c < 3; ++c) acc[c] += v[c];
+    }
+    block_scan3(sh, acc);
+    if (threadIdx.x == 255)
+#pragma unroll
+        for (int c = 0; c < 3; ++c) tsum[3 * blockIdx.x + c] = acc[c];
+}
+
+// one workgroup: exclusive scan of the ntiles totals in place
+__global__ __launch_bounds__(256) void serial_scan_totals_kernel(double *__restrict__ tsum, uint32_t ntiles) {
+    __shared__ double sh[3][256];
+    const uint32_t per = (ntiles + 255u) / 256u;
+    const uint32_t b = threadIdx.x * per, e = min(b + per, ntiles);
+    double acc[3] = {0.0, 0.0, 0.0};
+    for (uint32_t i = b; i < e; ++i)
+#pragma unroll
+        for (int c = 0; c < 3; ++c) acc[c] += tsum[3 * i + c];
+    double inc[3] = {acc[0], acc[1], acc[2]};
+    block_scan3(sh, inc);
+    double run[3];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) run[c] = inc[c] - acc[c];  // (exclusive: the sum before b)
+    if (threadIdx.x == 0)
+#pragma unroll
+        for (int c = 0; c < 3; ++c) run[c] = 0.0;
+    for (uint32_t i = b; i < e; ++i)
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            const double x = tsum[3 * i + c];
+            tsum[3 * i + c] = run[c];
+            run[c] += x;
+        }
+}
+
+__global__ __launch_bounds__(256) void serial_scan_apply_kernel(double *__restrict__ tab, uint32_t npix,
+                                                                uint32_t spp, const double *__restrict__ tsum) {
+    __shared__ double sh[3][256];
+    const uint32_t p0 = blockIdx.x * kScanTile + threadIdx.x * 4u;
+    double v[4][3], acc[3] = {0.0, 0.0, 0.0};
+    for (uint32_t k = 0; k < 4; ++k) {
+        scan_inputs(tab, npix, spp, p0 + k, v[k]);
+#pragma unroll
+        for (int c = 0; c < 3; ++c) acc[c] += v[k][c];
+    }
+    double inc[3] = {acc[0], acc[1], acc[2]};
+    block_scan3(sh, inc);
+    double run[3];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) run[c] = tsum[3 * blockIdx.x + c] + (inc[c] - acc[c]);
+    if (threadIdx.x == 0)
+#pragma unroll
+        for (int c = 0; c < 3; ++c) run[c] = tsum[3 * blockIdx.x + c];
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        tab[0] = 0.0;                         // P[0]
+        tab[2 * (size_t)npix + 1] = 0.0;      // PV[0]
+    }
+    for (uint32_t k = 0; k < 4; ++k) {
+        const uint32_t p = p0 + k;
+#pragma unroll
+        for (int c = 0; c < 3; ++c) run[c] += v[k][c];
+        if (p < npix) {
+            tab[p + 1] = run[0];
+            tab[2 * (size_t)npix + 2 + p] = run[1];
+            if (p + 1 == npix) tab[5 * (size_t)npix + 2] = run[2];  // sum of ss
+        }
+    }
+}
+
+// dmax over the window starts a = i q, q = max(1, L / 4) (atomicMax on the
+// bits of a non-negative double orders like the doubles), plus V(n0).
+__global__ __launch_bounds__(256) void serial_reach_kernel(double *__restrict__ tab, uint32_t npix, uint32_t spp,
+                                                           uint32_t L, uint32_t n0) {
+    const SerialPred m{tab, tab + npix + 1, spp, npix};
+    const uint32_t N = npix * spp;  // (< 2^32, runtime.cpp)
+    const uint32_t q = max(1u, L / 4u);
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    unsigned long long *dmax = reinterpret_cast<unsigned long long *>(tab + 5 * (size_t)npix + 3);
+    if (i * q < N) {
+        const uint32_t a = (uint32_t)(i * q);
+        const uint64_t e = (uint64_t)a + L + L / 4u;
+        const double d = serial_M(m, e < N ? (uint32_t)e : N) - serial_M(m, a);
+        atomicMax(dmax, (unsigned long long)__double_as_longlong(d > 0.0 ? d : 0.0));
+    }
+    if (i == 0) {
+        const double *PV = tab + 2 * (size_t)npix + 1, *var = tab + 3 * (size_t)npix + 2;
+        const uint32_t p = n0 / spp;
+        tab[5 * (size_t)npix + 4] = p < npix ? PV[p] + (double)(n0 - p * spp) * var[p] : PV[npix];
+    }
+}
+
+__global__ __launch_bounds__(256) void serial_check_count_kernel(const float *__restrict__ flags, uint32_t n,
+                                                                 unsigned long long *__restrict__ count) {
+    uint32_t c = 0;
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
+        c += flags[i] != 0.0f ? 1u : 0u;
+    for (uint32_t off = kWave / 2; off > 0; off >>= 1) c += __shfl_xor(c, (int)off);
+    if ((threadIdx.x & (kWave - 1u)) == 0 && c != 0) atomicAdd(count, (unsigned long long)c);
+}
+
+hipError_t launch_serial_check_count(const float *flags, uint32_t n, unsigned long long *count,
+                                     hipStream_t stream) {
+    if (!n) return hipSuccess;
+    const uint32_t want = (n + 255) / 256, blocks = want < 2048 ? want : 2048;
+    hipLaunchKernelGGL(serial_check_count_kernel, dim3(blocks), dim3(256), 0, stream, flags, n, count);
+    return hipGetLastError();
+}
+
+size_t serial_tab_doubles(uint32_t npix) { return 5 * (size_t)npix + 10; }
+
+size_t serial_scan_scratch(uint32_t npix) { return 3 * (size_t)((npix + kScanTile - 1) / kScanTile) + 3; }
+
+hipError_t launch_serial_moments(const float *est, uint32_t pix0, uint32_t n, uint32_t spp, uint32_t R,
+                                 double scale, double *tab, uint32_t npix, hipStream_t stream) {
+    if (!n) return hipSuccess;
+    hipLaunchKernelGGL(serial_moments_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, est, pix0, n, spp,
+                       R, scale, tab, npix);
+    return hipGetLastError();
+}
+
+hipError_t launch_serial_tables(double *tab, double *scratch, uint32_t npix, uint32_t spp, uint32_t L,
+                                uint32_t n0, hipStream_t stream) {
+    if (!npix) return hipSuccess;
+    const uint32_t ntiles = (npix + kScanTile - 1) / kScanTile;
+    hipLaunchKernelGGL(serial_scan_tiles_kernel, dim3(ntiles), dim3(256), 0, stream, tab, npix, spp, scratch);
+    hipLaunchKernelGGL(serial_scan_totals_kernel, dim3(1), dim3(256), 0, stream, scratch, ntiles);
+    hipLaunchKernelGGL(serial_scan_apply_kernel, dim3(ntiles), dim3(256), 0, stream, tab, npix, spp, scratch);
+    const uint32_t N = npix * spp, q = L / 4u > 1u ? L / 4u : 1u;
+    const uint64_t pts = ((uint64_t)N + q - 1) / q;
+    hipLaunchKernelGGL(serial_reach_kernel, dim3((uint32_t)((pts + 255) / 256)), dim3(256), 0, stream, tab,
+                       npix, spp, L, n0);
+    return hipGetLastError();
+}
+
 hipError_t launch_serial_window(const uint32_t *ctrl, const uint32_t *jump, uint32_t *win, uint32_t n,
                                 hipStream_t stream) {
     if (!n) return hipSuccess;
@@ -1615,7 +1824,7 @@ uint32_t serial_walk_block(uint32_t L) {
     return R < 32u ? 32u : R;
 }
 
-hipError_t launch_serial_walk(uint32_t *ctrl, const float *table, const double *M, const double *V,
+hipError_t launch_serial_walk(uint32_t *ctrl, const float *table, SerialPred M, const double *V,
                               uint32_t npix, uint32_t spp, float z, float sfloor, const uint32_t *win,
                               uint32_t *states, uint32_t *bend, uint32_t *path, uint32_t *fin, uint32_t L,
                               uint32_t K, uint32_t depth, uint32_t nserial, hipStream_t stream) {

@@ -53,8 +53,8 @@ DeviceState::~DeviceState() {
                     bvh_nodes, bvh_prims, big_hot, bvh_miss, bvh_prim_id, big_id, bvh_miss16,
                     sph_shade, sph_kind, tbvh_nodes, tbvh_tris, tbvh_loose,
                     cam_nodes, cam_tris, ptl_off, ptl_items, spl, tile, gath,
-                    sstates, sM, sV, swin, sjump, sctrl, sbend, spath, sfin,
-                    gspl, gspl_rects, gspl_flag};
+                    sstates, stab, sscan, swin, sjump, sctrl, sbend, spath, sfin,
+                    gspl, gspl_rects, gspl_flag, scheck};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
     for (hipEvent_t e : ev)
@@ -775,13 +775,8 @@ std::vector<uint32_t> xorshift_jump_table() {
 // sigma), scaled for the means' estimation error from `per` traces a pixel
 static double serial_floor(uint64_t per) { return 0.05 * std::sqrt(1.0 + 1.0 / (double)per); }
 
-int render_frame_serial(WorldState &w, const CameraModel &cam, size_t width, size_t height,
-                        const RtRenderOptions &o, uint32_t *d_out, hipStream_t stream,
-                        RtRenderStats *stats) {
-    if (stats) std::memset(stats, 0, sizeof(*stats));
-    if (width == 0 || height == 0) return 0;
-    const uint64_t spp = (uint64_t)std::max(o.samples_per_pixel, 0);
-    const uint64_t N = (uint64_t)width * height * spp;
+static int serial_check_args(size_t width, size_t height, const RtRenderOptions &o) {
+    const uint64_t N = (uint64_t)width * height * (uint64_t)std::max(o.samples_per_pixel, 0);
     if (N >= 0xFFFFFFFFull) {
         set_error("RT_RNG_SERIAL: width * height * spp must be below 2^32");
         return -1;
@@ -790,12 +785,20 @@ int render_frame_serial(WorldState &w, const CameraModel &cam, size_t width, siz
         set_error("RT_RNG_SERIAL: max_ray_bounces above 100000");
         return -1;
     }
+    return 0;
+}
+
+// Steps 1 and 2 of SERIAL mode on device d, stream s: every sample's start
+// state of the whole width x height frame into d->sstates (frame sample
+// order), the events sev[0] (start), sev[2] (tables done) and sev[1] (states
+// found) recorded on s; with RT_FLAG_SERIAL_CHECK the chain is checked after
+// sev[1].  stats (optional) gets the serial_* fields.
+static int serial_find_states(WorldState &w, const CameraModel &cam, size_t width, size_t height,
+                              const RtRenderOptions &o, DeviceState *d, hipStream_t s, RtRenderStats *stats) {
+    const uint64_t spp = (uint64_t)std::max(o.samples_per_pixel, 0);
+    const uint64_t N = (uint64_t)width * height * spp;
     const uint32_t depth = (uint32_t)std::max(o.max_ray_bounces, 0);
-    std::lock_guard<std::recursive_mutex> lock(w.mu);
-    DeviceState *d = nullptr;
-    int rc = device_for(w, o.device, d);
-    if (rc) return rc;
-    hipStream_t s = stream ? stream : d->stream;
+    int rc = 0;
     if (d->done_stream && d->done_stream != s) HIP_TRY(hipStreamWaitEvent(s, d->done, 0));
     HIP_TRY(hipEventRecord(d->sev[0], s));
     HIP_TRY(grow(d->sstates, d->sstates_cap, std::max<uint64_t>(N, 1)));
@@ -804,44 +807,52 @@ int render_frame_serial(WorldState &w, const CameraModel &cam, size_t width, siz
     ob.rank = 0;
     ob.nranks = 1;
     ob.flags = 0;
+    uint32_t final_state = o.seed;  // the stream state after the last sample
     if (N > 0) {
         const auto tp0 = std::chrono::steady_clock::now();  // (RT_AMD_SERIAL_DEBUG)
-        // 1. per-pixel mean scatter counts from R counter-seeded traces per sample
+        // 1. per-pixel mean scatter counts from R counter-seeded traces per
+        // sample, reduced on the device (per-pixel moments, then prefix sums
+        // over pixels): no per-sample table and no host pass over the samples
         const uint64_t R = std::max<uint64_t>(
             1, std::min<uint64_t>({(32 + spp - 1) / spp, 16, 0x7FFFFFFFull / N}));
         const uint64_t npix = (uint64_t)width * height;
-        std::vector<double> mu(npix, 0.0), sq(npix, 0.0);
-        double ss = 0.0;  // within-pixel sum of squares (sigma of one sample's b)
+        const double per = (double)(spp * R);
+        const uint64_t L = std::max<uint64_t>(1, std::min<uint64_t>(env_u64("RT_AMD_SERIAL_CHUNK", 16384), N));
+        const uint64_t n0 = std::min(N, L);
+        HIP_TRY(grow(d->stab, d->stab_cap, serial_tab_doubles((uint32_t)npix)));
+        HIP_TRY(grow(d->sscan, d->sscan_cap, serial_scan_scratch((uint32_t)npix)));
+        double *const sums = d->stab + 5 * npix + 2;  // {sum ss, dmax, V(n0), lost count}
+        HIP_TRY(hipMemsetAsync(sums, 0, 8 * sizeof(double), s));
         {
-            std::vector<float> est;
-            const uint64_t step = std::max<uint64_t>(1, (1ull << 28) / R);
-            for (uint64_t c0 = 0; c0 < N; c0 += step) {
-                const uint32_t n = (uint32_t)std::min<uint64_t>(step, N - c0);
-                const SerialPass sp{kRngSerialEstimate, (uint32_t)c0, n, (uint32_t)R, nullptr, nullptr,
-                                    nullptr};
+            // launches of whole pixels, <= 2^28 traces each
+            const uint64_t step_pix = std::max<uint64_t>(1, ((1ull << 28) / R) / spp);
+            for (uint64_t p0 = 0; p0 < npix; p0 += step_pix) {
+                const uint64_t np = std::min(step_pix, npix - p0);
+                const SerialPass sp{kRngSerialEstimate, (uint32_t)(p0 * spp), (uint32_t)(np * spp), (uint32_t)R,
+                                    nullptr, SerialPred{}, nullptr};
                 rc = render_frame(w, cam, width, height, ob, nullptr, s, nullptr, &sp);
                 if (rc) return rc;
-                est.resize((size_t)n * R);
-                HIP_TRY(hipMemcpyAsync(est.data(), d->samples, est.size() * 4, hipMemcpyDeviceToHost, s));
-                HIP_TRY(hipStreamSynchronize(s));
-                for (uint64_t i = 0; i < est.size(); ++i) {
-                    const float b = est[i];
-                    if (!(b >= 0.0f)) {
-                        set_error("RT_RNG_SERIAL: estimate pass lost a sample's draw count");
-                        return -5;
-                    }
-                    const uint64_t pix = (c0 + i / R) / spp;
-                    mu[pix] += b;
-                    sq[pix] += (double)b * b;
-                }
-            }
-            const double per = (double)(spp * R);
-            for (uint64_t q = 0; q < npix; ++q) {
-                mu[q] /= per;
-                ss += sq[q] - per * mu[q] * mu[q];
+                HIP_TRY(launch_serial_moments(d->samples, (uint32_t)p0, (uint32_t)np, (uint32_t)spp, (uint32_t)R,
+                                              1.0 + 1.0 / per, d->stab, (uint32_t)npix, s));
             }
         }
-        const double sigma = std::sqrt(std::max(ss, 0.0) / (double)(N * R)) + 0.05;
+        HIP_TRY(launch_serial_tables(d->stab, d->sscan, (uint32_t)npix, (uint32_t)spp, (uint32_t)L, (uint32_t)n0, s));
+        HIP_TRY(hipEventRecord(d->sev[2], s));
+        double sm[4];
+        HIP_TRY(hipMemcpyAsync(sm, sums, sizeof(sm), hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
+        if (sm[3] != 0.0) {
+            set_error("RT_RNG_SERIAL: estimate pass lost a sample's draw count");
+            return -5;
+        }
+        double dmax = 0.0;  // largest predicted offset within L + L/4 samples: the window
+        {
+            uint64_t bits;
+            std::memcpy(&bits, &sm[1], 8);
+            std::memcpy(&dmax, &bits, 8);
+        }
+        const double sigma = std::sqrt(std::max(sm[0], 0.0) / (double)(N * R)) + 0.05;
+        const SerialPred pred{d->stab, d->stab + npix + 1, (uint32_t)spp, (uint32_t)npix};
         // 2. iterations of L samples from the first unresolved one (ctrl[4]),
         // K candidates per sample, spanning +-z sigma of the deviation of the
         // true offset from the predicted one at the end of L samples.  Narrow
@@ -852,7 +863,6 @@ int render_frame_serial(WorldState &w, const CameraModel &cam, size_t width, siz
         // -> 103 / 9 / 126 ms, 4096 -> 71 / 7 / 85, 16384 -> 56 / 6 / 61, 65536 ->
         // 72 / 6 / 64; z 1.0 / 1.5 / 2.0 within 5 %: short iterations pay the
         // launch tail, long ones the sqrt(L) wider windows)
-        const uint64_t L = std::max<uint64_t>(1, std::min<uint64_t>(env_u64("RT_AMD_SERIAL_CHUNK", 16384), N));
         const double z = (double)env_u64("RT_AMD_SERIAL_Z10", 15) / 10.0;
         const double spread = std::sqrt((double)L * (1.0 + 1.0 / (double)(spp * R)));
         uint64_t K = (uint64_t)std::ceil(2.0 * z * sigma * spread) + 2 * (uint64_t)depth + 2;
@@ -863,50 +873,23 @@ int render_frame_serial(WorldState &w, const CameraModel &cam, size_t width, siz
             set_error("RT_RNG_SERIAL: candidate table too large");
             return -5;
         }
-        // prefix sums of the predicted per-sample scatter counts
-        std::vector<double> M(N + 1);
-        M[0] = 0.0;
-        for (uint64_t j = 0; j < N; ++j) M[j + 1] = M[j] + mu[j / spp];
-        // and of each sample's variance around it (the pixel's own, scaled for the
-        // means' estimation error): the walks size each iteration's windows
-        // from it, 2 z (sqrt(V) + 0.05 sqrt(n scale)) + 2 depth + 2 for n
-        // samples -- the frame-wide K above where every pixel has the frame's
-        // sigma, narrower over sky and other constant-count pixels
-        // (per pixel: V(j) = P[p] + (j - p spp) var[p] for sample j of pixel p,
-        // with P the prefix sums over pixels of spp var: npix + 1 and npix
-        // doubles instead of N + 1)
+        // The walks size each iteration's windows from the per-pixel variances
+        // (V: prefix sums over pixels of spp var, then var; the variance of
+        // samples [0, j) is PV[p] + (j - p spp) var[p]): 2 z (sqrt(V) + 0.05
+        // sqrt(n scale)) + 2 depth + 2 for n samples -- the frame-wide K above
+        // where every pixel has the frame's sigma, narrower over sky and other
+        // constant-count pixels
         const bool adapt = env_u64("RT_AMD_SERIAL_ADAPT", 1) != 0;
-        std::vector<double> V;  // [P (npix + 1) | var (npix)]
-        if (adapt) {
-            V.assign(2 * npix + 1, 0.0);
-            const double per = (double)(spp * R), scale = 1.0 + 1.0 / per;
-            for (uint64_t q = 0; q < npix; ++q) {
-                const double v = std::max(sq[q] / per - mu[q] * mu[q], 0.0) * scale;
-                V[npix + 1 + q] = v;
-                V[q + 1] = V[q] + (double)spp * v;
-            }
-        }
-        auto vsum = [&](uint64_t j) {  // V(j): variance of samples [0, j)
-            const uint64_t q = std::min<uint64_t>(j / spp, npix);
-            return q < npix ? V[q] + (double)(j - q * spp) * V[npix + 1 + q] : V[npix];
-        };
-        double dmax = 0.0;  // largest predicted offset within L samples: the window
-        for (uint64_t a = 0; a < N; a += std::max<uint64_t>(1, L / 4))
-            dmax = std::max(dmax, M[std::min(N, a + L + L / 4)] - M[a]);
+        const double *Vdev = d->stab + 2 * npix + 1;
         const uint64_t wlen = 2 * L + 3 * ((uint64_t)std::ceil(dmax) + K + (uint64_t)depth) + 8;
         if (wlen >= 0xFFFFFFFFull) {
             set_error("RT_RNG_SERIAL: candidate window too large");
             return -5;
         }
         const uint64_t R_walk = serial_walk_block((uint32_t)L);
-        HIP_TRY(grow(d->sM, d->sM_cap, N + 1));
-        HIP_TRY(hipMemcpyAsync(d->sM, M.data(), (N + 1) * 8, hipMemcpyHostToDevice, s));
         uint32_t K0 = 0;  // the first iteration's candidates (later ones: the walks)
         if (adapt) {
-            HIP_TRY(grow(d->sV, d->sV_cap, V.size()));
-            HIP_TRY(hipMemcpyAsync(d->sV, V.data(), V.size() * 8, hipMemcpyHostToDevice, s));
-            const uint64_t n0 = std::min(N, L);
-            const double w0 = 2.0 * z * (std::sqrt(vsum(n0)) + serial_floor(spp * R) * std::sqrt((double)n0));
+            const double w0 = 2.0 * z * (std::sqrt(std::max(sm[2], 0.0)) + serial_floor(spp * R) * std::sqrt((double)n0));
             K0 = (uint32_t)std::min<double>((double)K, std::ceil(w0) + 2.0 * depth + 2.0);
         }
         HIP_TRY(grow(d->swin, d->swin_cap, wlen));
@@ -946,11 +929,11 @@ int render_frame_serial(WorldState &w, const CameraModel &cam, size_t width, siz
             const auto t0 = std::chrono::steady_clock::now();
             for (uint64_t q = 0; q < it; ++q) {
                 HIP_TRY(launch_serial_window(d->sctrl, d->sjump, d->swin, (uint32_t)wlen, s));
-                const SerialPass sp{kRngSerialCount, 0u, (uint32_t)L, (uint32_t)K, d->swin, d->sM,
+                const SerialPass sp{kRngSerialCount, 0u, (uint32_t)L, (uint32_t)K, d->swin, pred,
                                     d->sctrl};
                 rc = render_frame(w, cam, width, height, ob, nullptr, s, nullptr, &sp);
                 if (rc) return rc;
-                HIP_TRY(launch_serial_walk(d->sctrl, d->samples, d->sM, adapt ? d->sV : nullptr,
+                HIP_TRY(launch_serial_walk(d->sctrl, d->samples, pred, adapt ? Vdev : nullptr,
                                            (uint32_t)npix, (uint32_t)spp, (float)z, (float)serial_floor(spp * R),
                                            d->swin, d->sstates, d->sbend, gather ? d->spath : nullptr,
                                            gather ? d->sfin : nullptr, (uint32_t)L, (uint32_t)K, depth,
@@ -963,7 +946,11 @@ int render_frame_serial(WorldState &w, const CameraModel &cam, size_t width, siz
             t_enqueue += std::chrono::duration<double, std::milli>(t1 - t0).count();
             t_wait += std::chrono::duration<double, std::milli>(t2 - t1).count();
         }
-        if (stats) stats->serial_retries = ctrl[6];
+        if (stats) {
+            stats->serial_retries = ctrl[6];
+            stats->serial_iterations = ctrl[3];
+        }
+        final_state = ctrl[1];
         if (dbg_ev[0]) {
             HIP_TRY(hipEventRecord(dbg_ev[1], s));
             HIP_TRY(hipEventSynchronize(dbg_ev[1]));
@@ -981,24 +968,90 @@ int render_frame_serial(WorldState &w, const CameraModel &cam, size_t width, siz
         }
     }
     HIP_TRY(hipEventRecord(d->sev[1], s));
+    if (N > 0 && (o.flags & RT_FLAG_SERIAL_CHECK)) {
+        // the chain the reference's one stream forms (common.rs:321-341):
+        // sample 0 starts at the seed, sample j ends where j + 1 starts,
+        // the last one where the search ended (ctrl[1])
+        if (const char *brk = std::getenv("RT_AMD_SERIAL_BREAK")) {
+            // (tests: corrupt one found start state, so the check must see the
+            // links into and out of that sample break)
+            const uint64_t j = std::strtoull(brk, nullptr, 10);
+            if (j < N) {
+                uint32_t x = 0;
+                HIP_TRY(hipMemcpyAsync(&x, d->sstates + j, 4, hipMemcpyDeviceToHost, s));
+                HIP_TRY(hipStreamSynchronize(s));
+                x = x == 1u ? 2u : 1u;
+                HIP_TRY(hipMemcpyAsync(d->sstates + j, &x, 4, hipMemcpyHostToDevice, s));
+                HIP_TRY(hipStreamSynchronize(s));
+            }
+        }
+        uint32_t first = 0;
+        HIP_TRY(hipMemcpyAsync(&first, d->sstates, 4, hipMemcpyDeviceToHost, s));
+        if (!d->scheck) HIP_TRY(hipMalloc((void **)&d->scheck, 8));
+        HIP_TRY(hipMemsetAsync(d->scheck, 0, 8, s));
+        const uint64_t step = 1ull << 28;
+        for (uint64_t c0 = 0; c0 < N; c0 += step) {
+            const uint32_t n = (uint32_t)std::min(step, N - c0);
+            const SerialPass sp{kRngSerialCheck, (uint32_t)c0, n, 1u, d->sstates, SerialPred{}, nullptr};
+            RtRenderOptions oc = ob;
+            oc.seed = final_state;
+            rc = render_frame(w, cam, width, height, oc, nullptr, s, nullptr, &sp);
+            if (rc) return rc;
+            HIP_TRY(launch_serial_check_count(d->samples, n, d->scheck, s));
+        }
+        unsigned long long breaks = 0;
+        HIP_TRY(hipMemcpyAsync(&breaks, d->scheck, 8, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
+        if (stats) {
+            stats->serial_checked = N;
+            stats->serial_chain_breaks = breaks + (first != o.seed ? 1u : 0u);
+        }
+    }
+    return 0;
+}
+
+int render_frame_serial(WorldState &w, const CameraModel &cam, size_t width, size_t height,
+                        const RtRenderOptions &o, uint32_t *d_out, hipStream_t stream,
+                        RtRenderStats *stats) {
+    if (stats) std::memset(stats, 0, sizeof(*stats));
+    if (width == 0 || height == 0) return 0;
+    int rc = serial_check_args(width, height, o);
+    if (rc) return rc;
+    std::lock_guard<std::recursive_mutex> lock(w.mu);
+    DeviceState *d = nullptr;
+    rc = device_for(w, o.device, d);
+    if (rc) return rc;
+    hipStream_t s = stream ? stream : d->stream;
+    rc = serial_find_states(w, cam, width, height, o, d, s, stats);
+    if (rc) return rc;
+    const uint64_t N = (uint64_t)width * height * (uint64_t)std::max(o.samples_per_pixel, 0);
     // 3. the frame (or rank's tile) from the start states
     RtRenderOptions orp = o;
     orp.rng_mode = RT_RNG_REPLAY;
     orp.replay_states = nullptr;
-    const uint32_t retries = stats ? stats->serial_retries : 0;
+    RtRenderStats keep{};
+    if (stats) keep = *stats;
     rc = render_frame(w, cam, width, height, orp, d_out, s, stats, nullptr, d->sstates);
     if (rc) return rc;
     if (stats) {
-        stats->serial_retries = retries;
+        stats->serial_retries = keep.serial_retries;
+        stats->serial_iterations = keep.serial_iterations;
+        stats->serial_checked = keep.serial_checked;
+        stats->serial_chain_breaks = keep.serial_chain_breaks;
         float ms = 0.0f;
         HIP_TRY(hipEventSynchronize(d->sev[1]));
         HIP_TRY(hipEventElapsedTime(&ms, d->sev[0], d->sev[1]));
         stats->serial_ms = ms;
+        if (N > 0) {
+            HIP_TRY(hipEventElapsedTime(&ms, d->sev[0], d->sev[2]));
+            stats->serial_setup_ms = ms;
+        }
     }
     return 0;
 }
 
 long read_samples(WorldState &w, int device, float *out, size_t n) {
+    std::lock_guard<std::recursive_mutex> lock(w.mu);  // (device_for may add a device)
     DeviceState *d = nullptr;
     int rc = device_for(w, device, d);
     if (rc) return rc;
@@ -1118,6 +1171,36 @@ int render_frame_multi(WorldState &w, const CameraModel &cam, size_t width, size
         HIP_TRY(hipSetDevice(devs[0]));
         HIP_TRY(grow(ds[0]->gath, ds[0]->gath_cap, n * max_rows * width));
     }
+    // SERIAL: the reference's one stream is a sequential dependency, so the
+    // start states are found once, on the first device, and broadcast over
+    // RCCL; every device then renders its row blocks from them (REPLAY)
+    const bool serial = o.rng_mode == RT_RNG_SERIAL;
+    RtRenderStats sst{};
+    if (serial) {
+        rc = serial_check_args(width, height, o);
+        if (rc) return rc;
+        HIP_TRY(hipSetDevice(devs[0]));
+        rc = serial_find_states(w, cam, width, height, o, ds[0], ss[0], stats ? &sst : nullptr);
+        if (rc) return rc;
+        const uint64_t N = (uint64_t)width * height * (uint64_t)std::max(o.samples_per_pixel, 0);
+        if (n > 1 && N > 0) {
+            for (uint32_t g = 1; g < n; ++g) {
+                HIP_TRY(hipSetDevice(devs[g]));
+                HIP_TRY(grow(ds[g]->sstates, ds[g]->sstates_cap, N));
+            }
+            NCCL_TRY(ncclGroupStart());
+            for (uint32_t g = 0; g < n; ++g) {
+                const ncclResult_t r = ncclBroadcast(ds[0]->sstates, ds[g]->sstates, N, ncclUint32, 0,
+                                                     (*comms)[g], ss[g]);
+                if (r != ncclSuccess) {
+                    (void)ncclGroupEnd();
+                    set_error(std::string("ncclBroadcast failed: ") + ncclGetErrorString(r));
+                    return -4;
+                }
+            }
+            NCCL_TRY(ncclGroupEnd());
+        }
+    }
     // every device renders its row blocks (asynchronously unless stats are
     // wanted: counters need a host wait per device)
     for (uint32_t g = 0; g < n; ++g) {
@@ -1127,8 +1210,14 @@ int render_frame_multi(WorldState &w, const CameraModel &cam, size_t width, size
         og.nranks = n;
         og.row_block = B;
         og.device = devs[g];
+        if (serial) {
+            og.rng_mode = RT_RNG_REPLAY;
+            og.replay_states = nullptr;
+        }
         RtRenderStats sg;
-        rc = render_frame(w, cam, width, height, og, ds[g]->tile, ss[g], stats ? &sg : nullptr);
+        HIP_TRY(hipSetDevice(devs[g]));
+        rc = render_frame(w, cam, width, height, og, ds[g]->tile, ss[g], stats ? &sg : nullptr, nullptr,
+                          serial ? ds[g]->sstates : nullptr);
         if (rc) return rc;
         if (stats) {
             stats->samples += sg.samples; stats->rays += sg.rays;
@@ -1150,9 +1239,15 @@ int render_frame_multi(WorldState &w, const CameraModel &cam, size_t width, size
     // device the tile is the frame and the gather lands in d_out directly
     const size_t bytes = max_rows * width * 4;
     NCCL_TRY(ncclGroupStart());
-    for (uint32_t g = 0; g < n; ++g)
-        NCCL_TRY(ncclGather(ds[g]->tile, n > 1 ? (void *)ds[0]->gath : (void *)d_out, bytes, ncclUint8,
-                            0, (*comms)[g], ss[g]));
+    for (uint32_t g = 0; g < n; ++g) {
+        const ncclResult_t r = ncclGather(ds[g]->tile, n > 1 ? (void *)ds[0]->gath : (void *)d_out, bytes,
+                                          ncclUint8, 0, (*comms)[g], ss[g]);
+        if (r != ncclSuccess) {
+            (void)ncclGroupEnd();  // (never leave this thread's group open)
+            set_error(std::string("ncclGather failed: ") + ncclGetErrorString(r));
+            return -4;
+        }
+    }
     NCCL_TRY(ncclGroupEnd());
     HIP_TRY(hipSetDevice(devs[0]));
     if (n > 1)
@@ -1165,7 +1260,38 @@ int render_frame_multi(WorldState &w, const CameraModel &cam, size_t width, size
         ds[g]->done_stream = ss[g];
     }
     HIP_TRY(hipSetDevice(devs[0]));
-    if (stats) HIP_TRY(hipStreamSynchronize(ss[0]));
+    if (stats) {
+        HIP_TRY(hipStreamSynchronize(ss[0]));
+        if (serial) {
+            stats->serial_retries = sst.serial_retries;
+            stats->serial_iterations = sst.serial_iterations;
+            stats->serial_checked = sst.serial_checked;
+            stats->serial_chain_breaks = sst.serial_chain_breaks;
+            float ms = 0.0f;
+            HIP_TRY(hipEventElapsedTime(&ms, ds[0]->sev[0], ds[0]->sev[1]));
+            stats->serial_ms = ms;
+            if (width * height * (size_t)std::max(o.samples_per_pixel, 0) > 0) {
+                HIP_TRY(hipEventElapsedTime(&ms, ds[0]->sev[0], ds[0]->sev[2]));
+                stats->serial_setup_ms = ms;
+            }
+        }
+    }
+    return 0;
+}
+
+int assemble_tiles(const uint32_t *gathered, uint32_t *out, size_t width, size_t height, uint32_t row_block,
+                   uint32_t nranks, size_t max_rows, hipStream_t stream) {
+    if (width == 0 || height == 0) return 0;
+    if (!gathered || !out) { set_error("rt_assemble_tiles: null buffer"); return -1; }
+    if (nranks == 0 || row_block == 0) { set_error("rt_assemble_tiles: nranks and row_block must be >= 1"); return -1; }
+    if (width > 0xFFFFFFu || height > 0xFFFFFFu) { set_error("frame too large"); return -1; }
+    for (uint32_t g = 0; g < nranks; ++g)
+        if (tile_rows(height, row_block, g, nranks) > max_rows) {
+            set_error("rt_assemble_tiles: max_rows is smaller than a rank's tile");
+            return -1;
+        }
+    HIP_TRY(launch_assemble(gathered, out, (uint32_t)width, (uint32_t)height, row_block, nranks,
+                            (uint32_t)max_rows, stream));
     return 0;
 }
 

@@ -11,6 +11,7 @@
 #include <string>
 
 #include "bvh.h"
+#include "render.h"
 #include "scene.h"
 
 struct RtRenderOptions;
@@ -28,7 +29,7 @@ struct DeviceState {
     int device = -1;
     hipStream_t stream = nullptr;
     hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
-    hipEvent_t sev[2] = {nullptr, nullptr};  // SERIAL mode: start-state search
+    hipEvent_t sev[3] = {nullptr, nullptr, nullptr};  // SERIAL mode: start, tables done, states found
     float4 *sph_hot = nullptr, *sph_cold = nullptr, *tri_hot = nullptr, *tri_geo = nullptr;
     float *mats = nullptr;
     float4 *sph_shade = nullptr;
@@ -69,14 +70,15 @@ struct DeviceState {
     // SERIAL mode (render_frame_serial): start states, candidate offsets, the
     // stream window of a chunk, xorshift jump matrices, control block
     uint32_t *sstates = nullptr;     size_t sstates_cap = 0;
-    double *sM = nullptr;            size_t sM_cap = 0;
-    double *sV = nullptr;            size_t sV_cap = 0;     // prefix sums of per-sample variances
+    double *stab = nullptr;          size_t stab_cap = 0;   // prediction tables (render.h serial_tab_doubles)
+    double *sscan = nullptr;         size_t sscan_cap = 0;  // their scan's scratch
     uint32_t *swin = nullptr;        size_t swin_cap = 0;
     uint32_t *sbend = nullptr;       size_t sbend_cap = 0;
     uint32_t *spath = nullptr;       size_t spath_cap = 0;  // block walks' paths (L x K)
     uint32_t *sfin = nullptr;                               // chain result (4 + 256)
     uint32_t *sjump = nullptr;
     uint32_t *sctrl = nullptr;
+    unsigned long long *scheck = nullptr;                       // chain-check count
     uint32_t *counter = nullptr;                                // job counter
     unsigned long long *stats = nullptr; size_t stats_cap = 0;  // per-wave counter records
     // resident workgroups per CU of each kernel variant, [0]: whole walks, [1]: sliced walks
@@ -125,7 +127,7 @@ struct SerialPass {
     uint32_t mode;            // kRngSerialCount or kRngSerialEstimate
     uint32_t cbase, nsamples, variants;
     const uint32_t *win;
-    const double *M;
+    SerialPred M;
     const uint32_t *ctrl;
 };
 
@@ -155,6 +157,11 @@ int render_frame_serial(WorldState &w, const CameraModel &cam, size_t width, siz
 int render_frame_multi(WorldState &w, const CameraModel &cam, size_t width, size_t height,
                        const RtRenderOptions &opts, uint32_t *d_out, hipStream_t stream,
                        RtRenderStats *stats);
+
+// assemble_kernel on its own (rt_assemble_tiles): checks the arguments
+// against the tile layout of tile_rows / tile_row, then launches.
+int assemble_tiles(const uint32_t *gathered, uint32_t *out, size_t width, size_t height, uint32_t row_block,
+                   uint32_t nranks, size_t max_rows, hipStream_t stream);
 
 // Ranks of the cached RCCL communicator of devices [first, first + n)
 // (created on first use), or a negative error.

@@ -21,6 +21,7 @@ LIB_PATH = os.environ.get("RT_AMD_LIB") or os.path.join(HERE, "lib", "libraytrac
 RNG_COUNTER, RNG_REPLAY, RNG_SERIAL = 1, 2, 3
 ACCEL_AUTO, ACCEL_BRUTE, ACCEL_BVH = 0, 1, 2
 FLAG_KEEP_SAMPLES = 1
+FLAG_SERIAL_CHECK = 2
 DEFAULT_SEED = 2547549
 
 # Every symbol declared in include/raytracer.h and include/raytracer_amd.h.
@@ -30,7 +31,7 @@ EXPORTS = (
     "rt_render_device", "rt_read_samples", "rt_free_world", "rt_last_error", "rt_world_num_spheres",
     "rt_world_num_triangles", "rt_world_sphere", "rt_world_triangle", "rt_camera_get",
     "rt_last_parse_error", "rt_write_ppm", "rt_device_count", "rt_comm_count",
-    "rt_world_set_sphere_material", "rt_world_set_triangle_material",
+    "rt_world_set_sphere_material", "rt_world_set_triangle_material", "rt_assemble_tiles",
 )
 
 
@@ -68,7 +69,9 @@ class RenderStats(C.Structure):
                 ("tri_node_tests", C.c_uint64), ("bvh_tri_tests", C.c_uint64),
                 ("tri_bvh", C.c_uint32), ("fused_resolve", C.c_uint32), ("serial_ms", C.c_double),
                 ("serial_retries", C.c_uint32), ("primary_lists", C.c_uint32),
-                ("camera_tree", C.c_uint32)]
+                ("camera_tree", C.c_uint32), ("serial_iterations", C.c_uint32),
+                ("serial_checked", C.c_uint64), ("serial_chain_breaks", C.c_uint64),
+                ("serial_setup_ms", C.c_double)]
 
     def as_dict(self):
         out = {}
@@ -143,6 +146,9 @@ def lib(path=None):
         L.rt_device_count.restype = C.c_int
         L.rt_comm_count.restype = C.c_int
         L.rt_comm_count.argtypes = [C.c_int, C.c_int]
+        L.rt_assemble_tiles.restype = C.c_int
+        L.rt_assemble_tiles.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_size_t, C.c_uint32,
+                                        C.c_uint32, C.c_size_t, C.c_void_p]
         _libs[path] = L
     return _libs[path]
 
@@ -164,6 +170,15 @@ def comm_count(first: int, n: int) -> int:
     return r
 
 
+def assemble_tiles(gathered_ptr: int, out_ptr: int, width, height, row_block, nranks, max_rows,
+                   stream_ptr: int = 0):
+    """rt_assemble_tiles: the multi-device frame assembly on device buffers."""
+    rc = lib().rt_assemble_tiles(C.c_void_p(gathered_ptr), C.c_void_p(out_ptr), width, height, row_block,
+                                 nranks, max_rows, C.c_void_p(stream_ptr or None))
+    if rc != 0:
+        raise RenderError(f"rt_assemble_tiles failed ({rc}): {last_error()}")
+
+
 def tile_rows(height, row_block, rank, nranks) -> int:
     return int(lib().rt_tile_rows(height, row_block, rank, nranks))
 
@@ -178,14 +193,14 @@ def sample_seed(seed: int, job: int) -> int:
 
 def options(spp=16, depth=8, mode=RNG_COUNTER, seed=DEFAULT_SEED, replay=None, row_block=8,
             rank=0, nranks=1, device=-1, accel=ACCEL_AUTO, keep_samples=False, L=None,
-            ndevices=0):
+            ndevices=0, serial_check=False):
     o = RenderOptions()
     (L or lib()).rt_default_options(C.byref(o))
     o.samples_per_pixel, o.max_ray_bounces, o.rng_mode, o.seed = spp, depth, mode, seed
     o.row_block, o.rank, o.nranks, o.device = row_block, rank, nranks, device
     o.accel = accel
     o.ndevices = ndevices
-    o.flags = FLAG_KEEP_SAMPLES if keep_samples else 0
+    o.flags = (FLAG_KEEP_SAMPLES if keep_samples else 0) | (FLAG_SERIAL_CHECK if serial_check else 0)
     keep = None
     if replay is not None:
         keep = np.ascontiguousarray(replay, dtype=np.uint32)
@@ -267,15 +282,16 @@ class World:
 
     def render(self, width, height, spp=16, depth=8, mode=RNG_COUNTER, seed=DEFAULT_SEED,
                replay=None, row_block=8, rank=0, nranks=1, device=-1, accel=ACCEL_AUTO,
-               keep_samples=False, stats=True, ndevices=0):
+               keep_samples=False, stats=True, ndevices=0, serial_check=False):
         """rt_render_ex -> (rgba uint8[tile_rows, width, 4], stats dict).
         keep_samples: write every sample to the slab (for read_samples) and
         resolve with the second kernel; the frame is bit-identical.
         stats=False: no counters (the kernel variant without them; stats None).
         ndevices >= 1: the whole frame, row-tiled over that many devices of this
-        process and gathered with RCCL (RtRenderOptions.ndevices)."""
+        process and gathered with RCCL (RtRenderOptions.ndevices).
+        serial_check: RT_FLAG_SERIAL_CHECK (SERIAL: verify the start-state chain)."""
         o, keep = options(spp, depth, mode, seed, replay, row_block, rank, nranks, device, accel,
-                          keep_samples, self._L, ndevices)
+                          keep_samples, self._L, ndevices, serial_check)
         rows = int(self._L.rt_tile_rows(height, row_block, rank, nranks)) if nranks > 1 else height
         px = np.zeros((rows, width, 4), np.uint8)
         fb = CFramebuffer(width, height, px.ctypes.data_as(C.POINTER(ColorU8)))
@@ -297,12 +313,13 @@ class World:
 
     def render_device(self, width, height, out_ptr: int, stream_ptr: int = 0, spp=16, depth=8,
                       mode=RNG_COUNTER, seed=DEFAULT_SEED, row_block=8, rank=0, nranks=1,
-                      device=-1, accel=ACCEL_AUTO, stats=True, keep_samples=False, ndevices=0):
+                      device=-1, accel=ACCEL_AUTO, stats=True, keep_samples=False, ndevices=0,
+                      serial_check=False):
         """rt_render_device into a device buffer (e.g. a torch uint8 tensor).
         stats=False: no counters and no host wait -- the frame is only enqueued
         on the stream (returns None)."""
         o, _ = options(spp, depth, mode, seed, None, row_block, rank, nranks, device, accel,
-                       keep_samples, self._L, ndevices)
+                       keep_samples, self._L, ndevices, serial_check)
         st = RenderStats()
         rc = self._L.rt_render_device(self._h, width, height, C.byref(o), C.c_void_p(out_ptr),
                                     C.c_void_p(stream_ptr or None), C.byref(st) if stats else None)

@@ -24,8 +24,7 @@ def _make(path):
 def built():
     """Build the oracle and the product library once (no-ops when up to date)."""
     _make(os.path.join(ROOT, "oracle"))
-    if not os.path.exists(os.path.join(PKG, "lib", "libraytracer.so")):
-        _make(PKG)
+    _make(PKG)  # (a no-op when the library is newer than its sources)
     return True
 
 

@@ -45,3 +45,24 @@ def test_c5_full_size_properties(mesh):
         t, tst = world.render(W, H, spp, depth, row_block=1, rank=q, nranks=H, accel=R.ACCEL_BRUTE)
         assert tst["tri_bvh"] == 0 and R.tile_row(0, 1, q, H) == q
         assert_bits_equal(a[q], t.reshape(-1, W, 4)[0], f"C5 image row {q} vs brute force")
+
+
+def test_c5_full_size_row_vs_oracle(mesh):
+    """Every 8th pixel of a C5 row at the full settings (64 spp, depth 8)
+    of the full-size frame, bit-compared with the oracle's brute-force
+    Mesh::hit (common.rs:177-224, every one of the 100k triangles per ray, in
+    file order) in COUNTER mode on 16 host threads: the phantom-aware trees,
+    camera records and strip lists of the GPU frame against the reference's
+    own loop at full size."""
+    import oracle as O
+
+    src, world = mesh
+    W, H, spp, depth = C5["W"], C5["H"], C5["spp"], C5["depth"]
+    a, _ = world.render(W, H, spp, depth, stats=False)
+    ref = O.Scene(src)
+    img = np.zeros((H, W, 4), np.uint8)
+    r = 300  # reference row (0 = bottom): image row 779, across the mesh wall
+    cols = slice(3, W, 8)  # every 8th pixel: 240 pixels x 64 samples (~10-20 s on 16 threads)
+    ref.render(W, H, spp, depth, mode=O.RNG_COUNTER, row_begin=r, row_step=H, col_begin=3, col_step=8,
+               nthreads=16, out=img)
+    assert_bits_equal(a[H - 1 - r, cols], img[H - 1 - r, cols], f"C5 reference row {r} vs oracle")

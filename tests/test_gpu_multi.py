@@ -120,3 +120,53 @@ def test_bench_torchrun_two_ranks_rehearsal():
     assert "verify: assembled frame == single-rank frame" in r.stderr
     line = json.loads(r.stdout.strip().splitlines()[-1])
     assert line["n_gpus"] == 2 and line["rccl_ranks"] == 2
+
+
+@pytest.mark.parametrize("n,h", [(2, 90), (3, 91), (8, 90), (8, 37), (3, 5), (5, 8)])
+def test_assemble_kernel_n_ranks(n, h):
+    """render_frame_multi's last step for n > 1 (which only a multi-GPU node
+    runs end to end): every rank's tile rendered on device 0, packed in the
+    layout the RCCL gather leaves on the first device (tile g at row g *
+    max_rows, short tiles padded), assembled by assemble_kernel through
+    rt_assemble_tiles, bit-identical to the single-device frame; also equal
+    to the host-side tiles.assemble.  Heights that are not multiples of the
+    8-row block, and more ranks than row blocks (3 x 5 rows)."""
+    import torch
+
+    import tiles
+
+    world = R.World(scene_text("rtow.txt"))
+    w, spp, B = 75, 2, 8
+    ref, _ = world.render(w, h, spp, 8)
+    max_rows = max(R.tile_rows(h, B, g, n) for g in range(n))
+    gathered = torch.full((n * max_rows * w * 4,), 7, dtype=torch.uint8, device="cuda:0")
+    for g in range(n):
+        rows = R.tile_rows(h, B, g, n)
+        if rows == 0:
+            continue
+        tile, _ = world.render(w, h, spp, 8, row_block=B, rank=g, nranks=n)
+        off = g * max_rows * w * 4
+        gathered[off:off + rows * w * 4] = torch.from_numpy(tile.reshape(-1)).to("cuda:0")
+    frame = torch.zeros(h * w * 4, dtype=torch.uint8, device="cuda:0")
+    R.assemble_tiles(gathered.data_ptr(), frame.data_ptr(), w, h, B, n, max_rows)
+    torch.cuda.synchronize(0)
+    out = frame.cpu().numpy().reshape(h, w, 4)
+    assert_bits_equal(out, ref, f"assembled {n}-rank frame")
+    host = tiles.assemble(gathered.cpu().numpy(), w, h, B, n)
+    assert_bits_equal(host, ref, f"tiles.assemble of the {n}-rank gather")
+    with pytest.raises(R.RenderError, match="max_rows"):
+        R.assemble_tiles(gathered.data_ptr(), frame.data_ptr(), w, h, B, n, max_rows - 1)
+
+
+def test_serial_multi_device_path_one_device():
+    """SERIAL through the multi-device path (render()'s default RNG with
+    RT_AMD_DEVICES): the start states are found once on the first device and
+    broadcast, then the tiles render in REPLAY mode -- bit-exact vs the
+    oracle's SERIAL frame."""
+    src = scene_text("c_raytracer_world.txt")
+    img, st, _ = O.Scene(src).render(48, 40, 4, 8, mode=O.RNG_SERIAL)
+    world = R.World(src)
+    out, gst = world.render(48, 40, 4, 8, mode=R.RNG_SERIAL, ndevices=1, serial_check=True)
+    assert_bits_equal(out, img, "ndevices=1 SERIAL frame")
+    assert gst["rays"] == st["rays"] and gst["serial_chain_breaks"] == 0 and gst["serial_checked"] == 48 * 40 * 4
+    assert gst["serial_ms"] > 0

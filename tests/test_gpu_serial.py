@@ -115,3 +115,56 @@ def test_serial_after_camera_move_and_counter_frames():
     img2, _, _ = ref.render(32, 24, 4, 8, mode=O.RNG_COUNTER)
     assert_bits_equal(cnt, img2, "COUNTER frame after SERIAL")
     assert not np.array_equal(cnt, out)
+
+
+def test_serial_large_frame_bit_exact():
+    """render()'s settings (16 spp, depth 8) at 960x540 on the
+    examples/c_raytracer.rs world -- 8.3 M samples of the one stream, about
+    650 candidate-table iterations -- bit-exact against the oracle's SERIAL
+    frame (~3 s of oracle time), with the chain check clean."""
+    src = scene_text("c_raytracer_world.txt")
+    img, st, out, gst, dt = _serial_pair(src, 960, 540, 16, 8, serial_check=True)
+    assert_bits_equal(out, img, "SERIAL 960x540x16 frame")
+    assert gst["rays"] == st["rays"]
+    assert gst["serial_checked"] == 960 * 540 * 16 and gst["serial_chain_breaks"] == 0
+    print(f"960x540x16/8 SERIAL: call {dt * 1e3:.0f} ms, start states {gst['serial_ms']:.0f} ms "
+          f"(tables {gst['serial_setup_ms']:.1f} ms, {gst['serial_iterations']} iterations)")
+
+
+@pytest.mark.parametrize("scene,w,h,spp", [
+    ("c_raytracer_world.txt", 1920, 1080, 16),  # render() at 1080p
+    ("rtow", 1920, 1080, 64),                   # BASELINE configs[1] (C2) settings
+])
+def test_serial_chain_full_size(scene, w, h, spp):
+    """Sizes the oracle cannot render in a test: the start states found on the
+    GPU form the reference's chain (sample 0 at the seed, every sample ending
+    where the next one starts, RT_FLAG_SERIAL_CHECK), and the frame is
+    deterministic.  With the trace arithmetic pinned bit-exact against the
+    oracle above, a closed chain from the seed is the reference's stream."""
+    src = S.rtow() if scene == "rtow" else scene_text(scene)
+    world = R.World(src)
+    t = time.perf_counter()
+    out, st = world.render(w, h, spp, 8, mode=R.RNG_SERIAL, serial_check=True)
+    dt = time.perf_counter() - t
+    assert st["serial_checked"] == w * h * spp
+    assert st["serial_chain_breaks"] == 0
+    assert (out[..., 3] == 255).all()
+    again, st2 = world.render(w, h, spp, 8, mode=R.RNG_SERIAL)
+    assert_bits_equal(again, out, "SERIAL frame rendered twice")
+    assert st2["rays"] == st["rays"]
+    print(f"{scene} {w}x{h}x{spp}/8 SERIAL: call {dt * 1e3:.0f} ms (with the check), start states "
+          f"{st2['serial_ms']:.0f} ms, {st2['serial_iterations']} iterations, "
+          f"{st2['rays'] / (st2['serial_ms'] + st2['trace_ms']) / 1e3:.1f} Mrays/s")
+
+
+def test_serial_chain_check_sees_a_corrupted_state(monkeypatch):
+    """The check is not vacuous: one corrupted start state breaks the link
+    into that sample and the link out of it (sample 0: the seed link)."""
+    src = scene_text("world.txt")
+    world = R.World(src)
+    _, st = world.render(40, 30, 4, 8, mode=R.RNG_SERIAL, serial_check=True)
+    assert st["serial_chain_breaks"] == 0
+    for j, want in ((777, 2), (0, 2), (40 * 30 * 4 - 1, 2)):
+        monkeypatch.setenv("RT_AMD_SERIAL_BREAK", str(j))
+        _, st = world.render(40, 30, 4, 8, mode=R.RNG_SERIAL, serial_check=True)
+        assert st["serial_chain_breaks"] == want, (j, st["serial_chain_breaks"])
