@@ -20,6 +20,7 @@ bounded row-cyclic sample of the same frame.
 from __future__ import annotations
 
 import argparse
+import hashlib
 import json
 import os
 import sys
@@ -396,11 +397,21 @@ def _report(args, src, world, W, H, spp, depth, st0, rays, elapsed, trace_ms, co
     achieved_tflops = flops_per_launch / (trace_ms * 1e-3) / 1e12
     alg_tflops = algorithmic_flops(st0) / launches / (trace_ms * 1e-3) / 1e12
     out_bytes = rows * W * 4
-    traffic = None
+    # roofline.traffic: HBM bytes per trace launch from the separate rocprofv3
+    # --pmc FETCH_SIZE / WRITE_SIZE passes of tools/profile.sh (counters cannot
+    # be read inside this run), reported with the profiled build's sha256 next
+    # to the sha256 of the library this run loaded
+    traffic, tsrc = None, None
     tfile = os.path.join(ROOT, "profiles", "hbm_traffic.json")
     if os.path.exists(tfile):
         with open(tfile) as fh:
-            traffic = json.load(fh).get(args.config, {}).get("trace_bytes_per_launch")
+            ent = json.load(fh).get(args.config, {})
+        traffic = ent.get("trace_bytes_per_launch")
+        with open(R.LIB_PATH, "rb") as fh:
+            loaded = hashlib.sha256(fh.read()).hexdigest()
+        tsrc = {"file": "profiles/hbm_traffic.json", "profile": ent.get("from"),
+                "profiled_lib_sha256": ent.get("lib_sha256"), "benched_lib_sha256": loaded,
+                "same_binary": ent.get("lib_sha256") == loaded}
     ms_per_step = elapsed / args.steps * 1e3
     result = {
         "metric": METRIC,
@@ -424,6 +435,7 @@ def _report(args, src, world, W, H, spp, depth, st0, rays, elapsed, trace_ms, co
         "roofline": {"bound": "valu", "achieved": achieved_tflops,
                      "peak": FP32_VECTOR_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": achieved_tflops / FP32_VECTOR_PEAK_TFLOPS, "traffic": traffic,
+                     "traffic_source": tsrc,
                      "kernel": "trace_kernel", "avg_launch_ms": trace_ms,
                      "counting_variant_ms": count_trace_ms,
                      "flops_per_launch": flops_per_launch, "flops": "executed work",

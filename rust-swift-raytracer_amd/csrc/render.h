@@ -110,6 +110,13 @@ struct TraceParams {
     float tbvh_oc[3];         // origin the boxes were built for (widening uses o - oc)
     float tq_base[3], tq_step[3], tq_nbase, tq_nstep;  // static-tree grids
     float cq_base[3], cq_step[3];                      // camera-tree grid
+    // per-cell top levels of the static tree (bvh.h TriangleBVH::top): nodes
+    // [0, tcell_top) of a ray whose origin lies in cell c are read from
+    // tcells[(c * tcell_top + node) * 2] and widened from the cell's centre
+    const uint4 *tcells;
+    uint32_t tcell_top;       // 0: no cells
+    float tcell_lo[3], tcell_size, tcell_inv;
+    uint32_t tcell_dim[3];
     // the same triangles' phantoms for the camera origin (bvh.h CameraTriangleBVH),
     // used at bounce 0; cam_nnodes == 0: bounce 0 uses the tree above
     const uint4 *cam_nodes;   // 2 per node: quantised box, a, link
@@ -137,6 +144,18 @@ struct TraceParams {
     uint32_t sspp;            // the frame's spp ...
     FastDiv div_sspp;         // ... and its divider
     uint32_t max_draws;       // 2 + 3 * max(depth, 0): bound of the draw count search
+    // kRngSerialCount chain mode (chain_mask != 0): the pool holds only the
+    // candidates of every (chain_mask + 1)-th sample; a lane that finishes
+    // candidate (jl, B) continues with (jl + 1, B + b) -- the one entry of the
+    // next sample the true path could take from there -- unless that entry is
+    // outside the window, starts a new run, or was claimed already (claim[]:
+    // one u32 per table entry, claimed by raising it to `tag`, the iteration's
+    // number).  Only the entries some path from a run's first sample reaches
+    // are traced; the walks read no others.
+    uint32_t *claim;
+    uint32_t chain_mask;      // run length - 1 (a power of two), 0 = every candidate
+    uint32_t nlaunch;         // chain mode: samples of the launch (p.npix = runs)
+    uint32_t tag;             // (set in the kernel: ctrl[7] + ctrl[3] + 1; ctrl[7] = 0)
 };
 
 // Candidate k of chunk sample jl (frame sample a + jl) means B = serial_lo + k

@@ -446,16 +446,20 @@ __device__ __forceinline__ bool tri_begin(const TraceParams &p, F3 org, F3 dir, 
 
 // One node of the triangle tree (static or camera-origin); an entered leaf is
 // handed back in `leaf` as (first << 3) | count, like sphere_node.
-__device__ __forceinline__ bool tri_node(const TraceParams &p, F3 nlo, F3 nhi, F3 inv, F3 dlt2, bool cam,
-                                         float cap, uint32_t &node, uint32_t &leaf,
-                                         uint32_t &node_tests) {
+// dlt2c, cbase, ctop: the ray's cell (tri_cell): nodes below ctop are read
+// from the cell's records at cbase and widened from its centre
+__device__ __forceinline__ bool tri_node(const TraceParams &p, F3 nlo, F3 nhi, F3 inv, F3 dlt2, F3 dlt2c,
+                                         uint32_t cbase, uint32_t ctop, bool cam, float cap,
+                                         uint32_t &node, uint32_t &leaf, uint32_t &node_tests) {
     ++node_tests;
     // Quantised nodes (bvh.h QuantGrid): u16 coordinates decoded with one fma
     // on the tree's grid; the host rounds every face outward *after* this
     // exact decode, so a decoded box contains the float box.
     // one 32-B sector per node: (static) box | normals | a | link,
     // (camera) box | a | link; fixed child-a-first order (bvh.cpp)
-    const uint4 *qn = (cam ? p.cam_nodes : p.tbvh_nodes) + 2u * node;
+    const bool top = node < ctop;
+    const uint4 *qn = cam ? p.cam_nodes + 2u * node : top ? p.tcells + 2u * (cbase + node) : p.tbvh_nodes + 2u * node;
+    const F3 dd = top ? dlt2c : dlt2;
     const uint4 q0 = qn[0], q1 = qn[1];
     const uint32_t a = cam ? q0.w : q1.z;
     const uint32_t miss = cam ? q1.x : q1.w;
@@ -480,9 +484,9 @@ __device__ __forceinline__ bool tri_node(const TraceParams &p, F3 nlo, F3 nhi, F
                                   __builtin_fmaf(hi16(q1.y), ns, nb), 0.0f);
     // 2s = n^.(2d) over the normal box, d = o - oc (the tree's box origin,
     // bvh.h); dlt2 = 2d is exact, so 2s m below has the bits of 2 (s m)
-    const float ax = N0.x * dlt2.x, bx = N1.x * dlt2.x;
-    const float ay = N0.y * dlt2.y, by = N1.y * dlt2.y;
-    const float az = N0.z * dlt2.z, bz = N1.z * dlt2.z;
+    const float ax = N0.x * dd.x, bx = N1.x * dd.x;
+    const float ay = N0.y * dd.y, by = N1.y * dd.y;
+    const float az = N0.z * dd.z, bz = N1.z * dd.z;
     const float sl = (fminf(ax, bx) + fminf(ay, by)) + fminf(az, bz);
     const float sh = (fmaxf(ax, bx) + fmaxf(ay, by)) + fmaxf(az, bz);
     // phantom offset 2 s m_k over 2s in [sl, sh], m_k in [N0.k, N1.k]
@@ -513,6 +517,32 @@ __device__ __forceinline__ bool tri_node(const TraceParams &p, F3 nlo, F3 nhi, F
     node = (skip || is_leaf) ? miss : child;
     leaf = a & ~kLeafBitDev;  // read only when the flag is set
     return !skip && is_leaf;
+}
+
+// The ray's cell for the static tree's top levels (bvh.h TriangleBVH::top):
+// any cell is exact (its boxes hold the phantoms for its centre c, widened by
+// the ray from c), the one holding the origin is the tightest.  Origins
+// outside the grid (and camera-tree lanes) get ctop = 0: static records only.
+// The centre is computed with the host's float operations (bvh.cpp).
+__device__ __forceinline__ void tri_cell(const TraceParams &p, F3 org, bool cam, F3 &dlt2c, uint32_t &cbase,
+                                         uint32_t &ctop) {
+    ctop = 0;
+    cbase = 0;
+    dlt2c = f3(0.0f, 0.0f, 0.0f);
+    if (cam || p.tcell_top == 0) return;
+    const float fx = floorf((org.x - p.tcell_lo[0]) * p.tcell_inv);
+    const float fy = floorf((org.y - p.tcell_lo[1]) * p.tcell_inv);
+    const float fz = floorf((org.z - p.tcell_lo[2]) * p.tcell_inv);
+    if (!(fx >= 0.0f && fx < (float)p.tcell_dim[0] && fy >= 0.0f && fy < (float)p.tcell_dim[1] &&
+          fz >= 0.0f && fz < (float)p.tcell_dim[2]))
+        return;
+    const uint32_t ix = (uint32_t)fx, iy = (uint32_t)fy, iz = (uint32_t)fz;
+    const float cx = p.tcell_lo[0] + ((float)ix + 0.5f) * p.tcell_size;
+    const float cy = p.tcell_lo[1] + ((float)iy + 0.5f) * p.tcell_size;
+    const float cz = p.tcell_lo[2] + ((float)iz + 0.5f) * p.tcell_size;
+    dlt2c = f3(2.0f * (org.x - cx), 2.0f * (org.y - cy), 2.0f * (org.z - cz));
+    cbase = ((ix * p.tcell_dim[1] + iy) * p.tcell_dim[2] + iz) * p.tcell_top;
+    ctop = p.tcell_top;
 }
 
 __device__ __forceinline__ void tri_leaf(const TraceParams &p, F3 org, F3 dir, bool cam,
@@ -552,13 +582,17 @@ __device__ __forceinline__ void job_pixel(const TraceParams &p, uint32_t job, ui
     row = p.height - 1u - ir;
 }
 
+// kRngSerialCount: the offset B (scatters since the iteration's first sample)
+// of job = launch sample jl * K + candidate k
+__device__ __forceinline__ uint32_t serial_offset(const TraceParams &p, uint32_t jl, uint32_t k) {
+    return serial_lo(p.sM, p.cbase, jl, p.spp, (p.max_draws - 2u) / 3u, p.nserial) + k;
+}
+
 // SERIAL passes: the start state of job (launch sample jl, variant k).
 __device__ __forceinline__ uint32_t serial_start(const TraceParams &p, uint32_t job) {
     const uint32_t jl = fdiv(job, p.div_spp);
     const uint32_t k = job - jl * p.spp;
-    if (p.mode == kRngSerialCount)
-        return p.win[2u * jl + 3u * (serial_lo(p.sM, p.cbase, jl, p.spp, (p.max_draws - 2u) / 3u,
-                                               p.nserial) + k)];
+    if (p.mode == kRngSerialCount) return p.win[2u * jl + 3u * serial_offset(p, jl, k)];
     if (p.mode == kRngSerialCheck) return p.win[p.cbase + jl];
     return counter_seed(p.seed, (uint64_t)(p.cbase + jl) * p.spp + k);
 }
@@ -706,12 +740,15 @@ void trace_kernel(TraceParams p) {
         p.cbase = p.ctrl[4];  // (the walks advance it)
         const uint32_t K = p.ctrl[5];
         if (p.mode == kRngSerialCount && K != 0u && K < p.spp) {
-            p.chunk = (p.chunk / K) * K;  // (whole samples, about as many jobs per atomic)
+            if (p.chain_mask == 0u) p.chunk = (p.chunk / K) * K;  // (whole samples, ~ as many jobs per atomic)
             p.spp = K;
             p.div_spp = make_fastdiv(K);
             p.njobs = p.npix * K;
         }
+        p.tag = p.ctrl[7] + p.ctrl[3] + 1u;
     }
+    // chain mode: a lane's next (sample, candidate) job, ~0u = none
+    uint32_t cont = ~0u;
     const uint32_t lane = __lane_id();
     extern __shared__ float4 lds[];
     BvhView view;
@@ -968,13 +1005,16 @@ void trace_kernel(TraceParams p) {
                 const bool cam = bounce == 0 && p.cam_nnodes != 0;
                 const F3 dlt2 = f3(2.0f * (org.x - p.tbvh_oc[0]), 2.0f * (org.y - p.tbvh_oc[1]),
                                    2.0f * (org.z - p.tbvh_oc[2]));
+                F3 dlt2c;
+                uint32_t cbase, ctop;
+                tri_cell(p, org, cam, dlt2c, cbase, ctop);
                 // rho (e; 0 on the camera tree) folded into the slab offsets
                 F3 nlo, nhi;
                 sphere_slabs(org, inv, e, nlo, nhi);
                 float cap = fminf(best_t, tri_t);
                 do {
                     uint32_t leaf;
-                    if (tri_node(p, nlo, nhi, inv, dlt2, cam, cap, node, leaf, tnode_tests)) {
+                    if (tri_node(p, nlo, nhi, inv, dlt2, dlt2c, cbase, ctop, cam, cap, node, leaf, tnode_tests)) {
                         tri_leaf(p, org, dir, cam, leaf, best_t, tri_t, tri_i, tri_in, tri_done);
                         cap = fminf(best_t, tri_t);
                     }
@@ -1082,11 +1122,29 @@ void trace_kernel(TraceParams p) {
                         ++n;
                     }
                     out_r = (x == rng && n >= 2u) ? (float)((n - 2u) / 3u) : -1.0f;
+                    if (p.chain_mask != 0u && p.mode == kRngSerialCount && out_r >= 0.0f) {
+                        // chain mode: the path from this entry goes on at (jl + 1,
+                        // B + b) -- traced by this lane unless another one got there
+                        // first (then both paths are one from here on)
+                        const uint32_t jl = fdiv(slot, p.div_spp);
+                        const uint32_t j1 = jl + 1u;
+                        if ((j1 & p.chain_mask) != 0u && j1 < p.nlaunch) {
+                            const uint32_t B1 = serial_offset(p, jl, slot - jl * p.spp) + (n - 2u) / 3u;
+                            const uint32_t l1 = serial_offset(p, j1, 0u);
+                            if (B1 >= l1 && B1 - l1 < p.spp) {
+                                const uint32_t e = j1 * p.spp + (B1 - l1);
+                                if (atomicMax(p.claim + e, p.tag) < p.tag) cont = e;
+                            }
+                        }
+                    }
                 }
-                // planar (R, G, B planes): 12 B per sample, to the slab or the ring
+                // planar (R, G, B planes): 12 B per sample, to the slab or the
+                // ring (SERIAL passes: plane 0 only)
                 sbase[slot] = out_r;
-                sbase[pstride + slot] = out_g;
-                sbase[2 * pstride + slot] = out_b;
+                if (!kSerial) {
+                    sbase[pstride + slot] = out_g;
+                    sbase[2 * pstride + slot] = out_b;
+                }
                 active = false;
             }
         }
@@ -1127,8 +1185,13 @@ void trace_kernel(TraceParams p) {
         // ---- refill lanes whose path ended (active-ray compaction) -------
         // (with the fused resolve a new chunk needs a free ring slot: with all
         // kTraceRing slots waiting on unfinished samples the lanes stay idle)
-        if (refill && !exhausted && !(fused && rfree == 0 && pool_next >= pool_end)) {
-            if (pool_next >= pool_end) {
+        // SERIAL chain mode: lanes whose path goes on take their next entry
+        // first, whatever the pool's state; the others take pool jobs
+        const uint64_t contm = kSerial ? __ballot(!active && cont != ~0u) : 0ull;
+        const uint64_t pdead = dead & ~contm;
+        const bool prefill = refill && !exhausted && !(fused && rfree == 0 && pool_next >= pool_end);
+        if (prefill || contm != 0ull) {
+            if (prefill && pool_next >= pool_end) {
                 uint32_t base = 0;
                 if (lane == 0) {
                     base = pbegin + (prefetch_pending ? prefetch
@@ -1168,11 +1231,22 @@ void trace_kernel(TraceParams p) {
                     }
                 }
             }
-            const uint32_t avail = pool_end - pool_next;
+            const uint32_t avail = prefill ? pool_end - pool_next : 0u;
             const uint32_t rank = __builtin_amdgcn_mbcnt_hi(
-                (uint32_t)(dead >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)dead, 0u));
-            if (!active && rank < avail) {
-                const uint32_t job = pool_next + rank;
+                (uint32_t)(pdead >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)pdead, 0u));
+            const bool own = kSerial && cont != ~0u;  // (only !active lanes hold one)
+            if (own || (!active && rank < avail)) {
+                uint32_t job = pool_next + rank;
+                if (kSerial) {
+                    if (own) {
+                        job = cont;
+                        cont = ~0u;
+                    } else if (p.chain_mask != 0u) {
+                        // pool job q = run r's candidate k -> job of sample r * run
+                        const uint32_t r = fdiv(job, p.div_spp);
+                        job = r * ((p.chain_mask + 1u) * p.spp) + (job - r * p.spp);
+                    }
+                }
                 // Jobs are enumerated pixel-major (job = pixel*spp + s): the
                 // lanes refilled together trace samples of one pixel (or of
                 // neighbours), so their primary walks visit the same nodes
@@ -1224,10 +1298,10 @@ void trace_kernel(TraceParams p) {
                 phase = kSetup;
                 active = true;
             }
-            pool_next += min(ndead, avail);
+            pool_next += min((uint32_t)__popcll(pdead), avail);
             // ask for the next chunk now; the reply is only waited for when the
             // pool runs dry (hides the ~1-3 us atomic round trip)
-            if (!exhausted && !prefetch_pending && pool_end - pool_next < kWave) {
+            if (prefill && !exhausted && !prefetch_pending && pool_end - pool_next < kWave) {
                 if (lane == 0) prefetch = atomicAdd(p.job_counter + 32u * part, p.chunk);
                 prefetch_pending = true;
             }

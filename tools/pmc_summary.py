@@ -33,6 +33,10 @@ def short(name):
 def main(src, dst, config="c2"):
     os.makedirs(dst, exist_ok=True)
     out = {"source": os.path.basename(src.rstrip("/")), "kernels": {}}
+    sha = os.path.join(src, "lib_sha256.txt")
+    if os.path.exists(sha):
+        out["lib_sha256"] = open(sha).read().strip()
+        shutil.copy(sha, os.path.join(dst, "lib_sha256.txt"))
     stats = glob.glob(os.path.join(src, "trace", "*kernel_stats.csv"))
     if stats:
         shutil.copy(stats[0], os.path.join(dst, "kernel_stats.csv"))
@@ -61,7 +65,8 @@ def main(src, dst, config="c2"):
         path = os.path.join(os.path.dirname(dst.rstrip("/")), "hbm_traffic.json")
         allc = json.load(open(path)) if os.path.exists(path) else {}
         allc[config] = {"trace_bytes_per_launch": tr["hbm_bytes_per_launch"],
-                        "from": os.path.relpath(dst, os.path.dirname(path))}
+                        "from": os.path.relpath(dst, os.path.dirname(path)),
+                        "lib_sha256": out.get("lib_sha256")}
         with open(path, "w") as fh:
             json.dump(allc, fh, indent=1)
     print(json.dumps(out, indent=1))

@@ -6,11 +6,13 @@ TAG=${1:-r01}; shift
 REPO="${GRAFT_REPO_ROOT:-/root/repo}"
 OUT="$REPO/gpurun_out/prof_$TAG"
 mkdir -p "$OUT"
+# the binary these counters describe (bench.py compares it with the one it loads)
+sha256sum "$REPO/rust-swift-raytracer_amd/lib/libraytracer.so" | cut -d' ' -f1 > "$OUT/lib_sha256.txt"
 cd /tmp && export TMPDIR=/tmp
 run() {  # run <name> <secs> <rocprof args...>
     local name=$1 secs=$2; shift 2
     timeout -k 10 "$secs" rocprofv3 "$@" -d "$OUT/$name" -o "$name" --output-format csv \
-        -- python3 "$REPO/bench.py" --no-cpu-baseline "${BENCH_ARGS[@]}" > "$OUT/$name.log" 2>&1
+        -- python3 "$REPO/bench.py" --no-cpu-baseline --no-serial "${BENCH_ARGS[@]}" > "$OUT/$name.log" 2>&1
     local rc=$?
     echo "$name rc=$rc"; tail -2 "$OUT/$name.log"
     [ $rc -eq 0 ] || exit $rc

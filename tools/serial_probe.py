@@ -31,14 +31,19 @@ def _cases():
         yield name, _scene(name), w, h, spp, int(depth)
 
 
-for name, s, w, h, spp, depth in _cases():
-    world = R.World(s)
-    world.render(w, h, spp, depth)  # device init
-    for k in range(int(os.environ.get("REPS", "2"))):
-        t = time.perf_counter()
-        _, st = world.render(w, h, spp, depth, mode=R.RNG_SERIAL)
-        dt = time.perf_counter() - t
-        n = w * h * spp
-        print(f"{name} {w}x{h}x{spp}/{depth}: call {dt * 1e3:.1f} ms, states {st['serial_ms']:.1f} ms, "
-              f"replay {st['trace_ms']:.2f} ms, retries {st['serial_retries']}, "
-              f"{st['rays'] / dt / 1e6:.1f} Mrays/s, {n / dt / 1e6:.1f} Msamples/s", flush=True)
+def main():
+    for name, s, w, h, spp, depth in _cases():
+        world = R.World(s)
+        world.render(w, h, spp, depth)  # device init
+        for k in range(int(os.environ.get("REPS", "2"))):
+            t = time.perf_counter()
+            _, st = world.render(w, h, spp, depth, mode=R.RNG_SERIAL)
+            dt = time.perf_counter() - t
+            n = w * h * spp
+            print(f"{name} {w}x{h}x{spp}/{depth}: call {dt * 1e3:.1f} ms, states {st['serial_ms']:.1f} ms, "
+                  f"replay {st['trace_ms']:.2f} ms, retries {st['serial_retries']}, "
+                  f"{st['rays'] / dt / 1e6:.1f} Mrays/s, {n / dt / 1e6:.1f} Msamples/s", flush=True)
+
+
+if __name__ == "__main__":
+    main()

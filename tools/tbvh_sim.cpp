@@ -50,6 +50,7 @@ static std::vector<int> g_depth;          // node depth (kernel image), for SIM_
 static std::vector<double> g_level_visits;
 
 static bool g_exact = false;
+static std::vector<uint32_t> *g_visits = nullptr;  // SIM_WAVE: the nodes a ray visits, in order
 static int g_hyb_D = 0;                       // SIM_HYB=D,S: per-cell boxes for depth < D
 static const std::vector<float> *g_cellbox = nullptr;  // 6 per node (lo, hi) for this ray's cell
 static double g_hyb_hits = 0;
@@ -72,6 +73,7 @@ static float trace(const TriangleBVH &t, V o, V d, Count &c) {
     uint32_t node = 0;
     while (node != kNodeEnd) {
         c.nodes += 1;
+        if (g_visits) g_visits->push_back(node);
         if (!g_depth.empty()) g_level_visits[g_depth[node]] += 1;
         const uint32_t *w = &t.qnodes[(size_t)node * 8];
         const uint32_t u[6] = {w[0] & 0xFFFF, w[0] >> 16, w[1] & 0xFFFF, w[1] >> 16, w[2] & 0xFFFF, w[2] >> 16};
@@ -439,6 +441,81 @@ int main(int argc, char **argv) {
                 }
             }
         }
+    if (const char *ws = std::getenv("SIM_WAVE")) {
+        // Wave coherence of secondary rays: groups of G rays whose origins are
+        // the hits of G jittered primary rays of one pixel (a wave's lanes hold
+        // samples of one or two pixels), directions random.  Per group: lane
+        // visits summed, the longest walk, the distinct nodes the lanes touch
+        // at each lockstep step (vector loads: one L2 request per distinct
+        // 32-B node per instruction), and the union of the walks (a wave-wide
+        // packet walk in DFS preorder: one scalar load per node of the union).
+        const int G = std::max(1, std::atoi(ws));
+        const size_t n = t.qnodes.size() / 8;
+        std::vector<uint32_t> rank(n, 0);  // preorder rank of each node
+        {
+            std::vector<uint32_t> st{0};
+            uint32_t r = 0;
+            while (!st.empty()) {
+                const uint32_t i = st.back(); st.pop_back();
+                rank[i] = r++;
+                const uint32_t a = t.qnodes[(size_t)i * 8 + 6];
+                if (!(a & kLeafBit)) { const uint32_t c = a & 0x1FFFFFFFu; st.push_back(c + 1); st.push_back(c); }
+            }
+        }
+        const bool cosine = std::getenv("SIM_WAVE_COS") != nullptr;  // normal + unit (diffuse) dirs
+        uint32_t rng3 = 12345u;
+        auto rnd3 = [&]() { rng3 ^= rng3 << 13; rng3 ^= rng3 >> 17; rng3 ^= rng3 << 5; return rng3 * 0x1p-32f; };
+        double lanes = 0, maxl = 0, uniq = 0, uni = 0, groups = 0, nonmono = 0;
+        Count dummy, wc;
+        for (int j = 0; j < H; ++j)
+            for (int i = 0; i < W; ++i) {
+                std::vector<std::vector<uint32_t>> walks;
+                for (int k = 0; k < G; ++k) {
+                    const float u = (i + rnd3()) / W, v = (j + rnd3()) / H;
+                    V d = unit(sub(add(add(V{cm.lower_left.x, cm.lower_left.y, cm.lower_left.z},
+                                           mul(V{cm.horizontal.x, cm.horizontal.y, cm.horizontal.z}, u)),
+                                       mul(V{cm.vertical.x, cm.vertical.y, cm.vertical.z}, v)), org));
+                    const float tt = trace(t, org, d, dummy);
+                    if (!std::isfinite(tt)) continue;
+                    V o2 = add(org, mul(d, tt));
+                    V d2 = unit(V{rnd3() * 2 - 1, rnd3() * 2 - 1, rnd3() * 2 - 1});
+                    if (cosine) {
+                        // around the nearest triangle's normal facing the ray origin side
+                        V nz{0, 0, 1};
+                        d2 = unit(add(nz, d2));
+                    }
+                    std::vector<uint32_t> vis;
+                    g_visits = &vis;
+                    trace(t, o2, d2, wc);
+                    g_visits = nullptr;
+                    walks.push_back(std::move(vis));
+                }
+                if (walks.empty()) continue;
+                groups += 1;
+                size_t mx = 0;
+                std::vector<uint32_t> all;
+                for (auto &w : walks) {
+                    lanes += w.size();
+                    mx = std::max(mx, w.size());
+                    for (size_t q = 1; q < w.size(); ++q) nonmono += rank[w[q]] <= rank[w[q - 1]];
+                    all.insert(all.end(), w.begin(), w.end());
+                }
+                maxl += mx;
+                for (size_t s = 0; s < mx; ++s) {
+                    std::vector<uint32_t> at;
+                    for (auto &w : walks) if (s < w.size()) at.push_back(w[s]);
+                    std::sort(at.begin(), at.end());
+                    uniq += std::unique(at.begin(), at.end()) - at.begin();
+                }
+                std::sort(all.begin(), all.end());
+                uni += std::unique(all.begin(), all.end()) - all.begin();
+            }
+        std::printf("waves of %d secondary rays (%s dirs): %.0f groups, per group: lane visits %.0f, longest "
+                    "walk %.0f, lockstep distinct nodes %.0f, union %.0f (non-monotone steps %.0f)\n",
+                    G, cosine ? "+z diffuse" : "uniform", groups, lanes / groups, maxl / groups, uniq / groups,
+                    uni / groups, nonmono);
+        return 0;
+    }
     if (const char *hs = std::getenv("SIM_HYB")) {
         float S = 1; std::sscanf(hs, "%d,%f", &g_hyb_D, &S);
         g_hyb_range = std::getenv("SIM_HYB_RANGE") != nullptr;
