@@ -369,14 +369,10 @@ static uint32_t node_word(const float *lo_a, const float *hi_b) {  // a, b bits 
 // (tools/tbvh_sim.cpp SIM_FIXED_OCT) but cost a second cache line per step.
 static void quantize_boxes(const std::vector<float> &nodes, size_t stride, bool normals,
                            const std::vector<uint32_t> &miss, std::vector<uint32_t> &q, QuantGrid &g,
-                           float *nbase, float *nstep, const float *cover = nullptr) {
+                           float *nbase, float *nstep) {
     const size_t n = nodes.size() / stride;
     float lo[3], hi[3], nlo = 1, nhi = -1;
     for (int k = 0; k < 3; ++k) { lo[k] = nodes[k]; hi[k] = nodes[4 + k]; }  // root holds all
-    for (int k = 0; cover && k < 3; ++k) {  // (a box the grid must also cover: the cells')
-        lo[k] = std::min(lo[k], cover[k]);
-        hi[k] = std::max(hi[k], cover[3 + k]);
-    }
     for (size_t i = 0; i < n && normals; ++i)
         for (int k = 0; k < 3; ++k) {
             nlo = std::min(nlo, nodes[i * stride + 8 + k]);
@@ -412,157 +408,6 @@ static void quantize_boxes(const std::vector<float> &nodes, size_t stride, bool 
             w[4] = miss[i * 8];
         }
     }
-}
-
-// Per-cell top levels (bvh.h TriangleBVH::top).  Renumbers out.nodes /
-// out.miss so that the nodes above depth `levels` come first in breadth-first
-// order (sibling pairs stay adjacent; the nodes below keep the builder order),
-// then builds, for every cell of a grid over `geo` (the triangles' box), the
-// boxes of those top nodes for the phantoms of the cell's centre c: each
-// triangle's padded box (triangle_prim) moved by 2(n^.c)n^, exactly in double,
-// the union over the node's triangles (a subtree covers a contiguous prim
-// range), rounded outward to float.  cover: the box of every cell's root.
-// RT_AMD_TRI_CELL_LEVELS (default 12, 0 = off), RT_AMD_TRI_CELLS (cells
-// along the box's longest axis, default 12).
-static void cell_top_levels(TriangleBVH &out, const std::vector<Prim> &prims, const Box &geo,
-                            std::vector<float> &cell_boxes, float cover[6]) {
-    const char *lv = std::getenv("RT_AMD_TRI_CELL_LEVELS");
-    const uint32_t levels = lv ? (uint32_t)std::min(16L, std::max(0L, std::strtol(lv, nullptr, 10))) : 0u;
-    const size_t n = out.nodes.size() / 16;
-    if (levels == 0 || n < 3) return;
-    auto a_of = [&](size_t i) { uint32_t a; std::memcpy(&a, &out.nodes[i * 16 + 3], 4); return a; };
-    auto b_of = [&](size_t i) { uint32_t b; std::memcpy(&b, &out.nodes[i * 16 + 7], 4); return b; };
-    // breadth-first order of the top levels
-    std::vector<uint32_t> order{0}, depth(n, 0);
-    for (size_t h = 0; h < order.size(); ++h) {
-        const uint32_t i = order[h];
-        const uint32_t a = a_of(i);
-        if ((a & kLeafBit) || depth[i] + 1 >= levels) continue;
-        depth[a] = depth[a + 1] = depth[i] + 1;
-        order.push_back(a);
-        order.push_back(a + 1);
-    }
-    const uint32_t top = (uint32_t)order.size();
-    if (top < 3 || top >= n) return;
-    std::vector<uint32_t> newid(n, kNodeEnd);
-    for (uint32_t k = 0; k < top; ++k) newid[order[k]] = k;
-    uint32_t next = top;
-    for (size_t i = 0; i < n; ++i)
-        if (newid[i] == kNodeEnd) newid[i] = next++;
-    std::vector<float> nodes(out.nodes.size());
-    std::vector<uint32_t> miss(out.miss.size());
-    for (size_t i = 0; i < n; ++i) {
-        float *o = &nodes[(size_t)newid[i] * 16];
-        std::memcpy(o, &out.nodes[i * 16], 16 * sizeof(float));
-        const uint32_t a = a_of(i);
-        if (!(a & kLeafBit)) {
-            const uint32_t c = newid[a];
-            if (newid[a + 1] != c + 1) return;  // (siblings always stay adjacent)
-            std::memcpy(&o[3], &c, 4);
-        }
-        for (int k = 0; k < 8; ++k) {
-            const uint32_t m = out.miss[i * 8 + k];
-            miss[(size_t)newid[i] * 8 + k] = m == kNodeEnd ? kNodeEnd : newid[m];
-        }
-    }
-    out.nodes.swap(nodes);
-    out.miss.swap(miss);
-    // prim range of every node, bottom-up: children follow their parent in
-    // both parts of the order (breadth-first on top, builder order below),
-    // and the left child holds the lower part of the parent's range
-    std::vector<uint32_t> first(n), count(n);
-    for (size_t i = n; i-- > 0;) {
-        const uint32_t a = a_of(i);
-        if (a & kLeafBit) { first[i] = a & ~kLeafBit; count[i] = b_of(i); continue; }
-        first[i] = first[a];
-        count[i] = count[a] + count[a + 1];
-    }
-    // the grid: cells of side S over geo, one cell of margin on each side
-    const char *ce = std::getenv("RT_AMD_TRI_CELLS");
-    const double per_axis = ce ? std::max(1.0, std::atof(ce)) : 12.0;
-    double ext = 0;
-    for (int k = 0; k < 3; ++k) ext = std::max(ext, geo.hi[k] - geo.lo[k]);
-    if (!(ext > 0) || !std::isfinite(ext)) return;
-    float S = up(ext / per_axis);
-    uint32_t dim[3];
-    float lo[3];
-    for (;;) {
-        size_t cells = 1;
-        for (int k = 0; k < 3; ++k) {
-            lo[k] = down(geo.lo[k] - S);
-            dim[k] = (uint32_t)std::ceil((geo.hi[k] + S - (double)lo[k]) / S);
-            cells *= dim[k];
-        }
-        // (at most 128 MB of records)
-        if (cells * top * 32 <= (128u << 20) && cells <= 65536) break;
-        S *= 1.25f;
-    }
-    const size_t ncell = (size_t)dim[0] * dim[1] * dim[2];
-    cell_boxes.assign(ncell * top * 6, 0.0f);
-    // frontier: top nodes whose children are below the top levels (or leaves)
-    std::vector<uint32_t> frontier;
-    for (uint32_t i = 0; i < top; ++i) {
-        const uint32_t a = a_of(i);
-        if ((a & kLeafBit) || a >= top) frontier.push_back(i);
-    }
-    std::vector<Box> roots(ncell);
-    auto build_cell = [&](size_t c) {
-        const uint32_t ci = (uint32_t)(c / ((size_t)dim[1] * dim[2]));
-        const uint32_t cj = (uint32_t)(c / dim[2] % dim[1]);
-        const uint32_t ck = (uint32_t)(c % dim[2]);
-        // the centre in float, as the kernel computes it
-        const float cf[3] = {lo[0] + ((float)ci + 0.5f) * S, lo[1] + ((float)cj + 0.5f) * S,
-                             lo[2] + ((float)ck + 0.5f) * S};
-        std::vector<Box> bx(top);
-        for (uint32_t f : frontier) {
-            Box b;
-            for (uint32_t j = first[f]; j < first[f] + count[f]; ++j) {
-                const Prim &p = prims[j];
-                const double s = p.n[0] * cf[0] + p.n[1] * cf[1] + p.n[2] * cf[2];
-                Box q = p.box;
-                for (int k = 0; k < 3; ++k) {
-                    q.lo[k] += 2 * s * p.n[k];
-                    q.hi[k] += 2 * s * p.n[k];
-                }
-                b.grow(q);
-            }
-            bx[f] = b;
-        }
-        for (uint32_t i = top; i-- > 0;) {
-            const uint32_t a = a_of(i);
-            if ((a & kLeafBit) || a >= top) continue;
-            bx[i] = bx[a];
-            bx[i].grow(bx[a + 1]);
-        }
-        for (uint32_t i = 0; i < top; ++i) {
-            float *o = &cell_boxes[(c * top + i) * 6];
-            for (int k = 0; k < 3; ++k) {
-                o[k] = down(bx[i].lo[k]);
-                o[3 + k] = up(bx[i].hi[k]);
-            }
-        }
-        roots[c] = bx[0];
-    };
-    unsigned hw = std::thread::hardware_concurrency();
-    const unsigned threads = std::min(16u, std::max(1u, hw));
-    std::atomic<size_t> cur{0};
-    auto work = [&]() {
-        for (size_t c; (c = cur.fetch_add(1)) < ncell;) build_cell(c);
-    };
-    std::vector<std::thread> pool;
-    for (unsigned t = 1; t < threads; ++t) pool.emplace_back(work);
-    work();
-    for (auto &t : pool) t.join();
-    Box all;
-    for (const Box &r : roots) all.grow(r);
-    for (int k = 0; k < 3; ++k) {
-        cover[k] = down(all.lo[k]);
-        cover[3 + k] = up(all.hi[k]);
-        out.cell_lo[k] = lo[k];
-        out.cell_dim[k] = dim[k];
-    }
-    out.cell_size = S;
-    out.top = top;
 }
 
 TriangleBVH build_triangle_bvh(const std::vector<Triangle> &tris, const std::vector<float> &tri_hot,
@@ -643,32 +488,7 @@ TriangleBVH build_triangle_bvh(const std::vector<Triangle> &tris, const std::vec
     out.miss.assign(b.nodes.size() * 8, kNodeEnd);
     for (uint32_t oct = 0; oct < 8; ++oct) b.links(0, kNodeEnd, oct, out.miss);
     out.tris = triangle_records(prims, tris, tri_hot);
-    std::vector<float> cell_boxes;  // cells x top x 6 (lo, hi), rounded outward
-    float cover[6];
-    if (!oc) cell_top_levels(out, prims, all, cell_boxes, cover);
-    quantize_boxes(out.nodes, 16, true, out.miss, out.qnodes, out.qbox, &out.nbase, &out.nstep,
-                   out.top ? cover : nullptr);
-    if (out.top) {
-        // a cell's record: its box on the static grid, the static record's
-        // normal box, child word and link
-        const size_t ncell = (size_t)out.cell_dim[0] * out.cell_dim[1] * out.cell_dim[2];
-        out.cell_qnodes.assign(ncell * out.top * 8, 0);
-        const QuantGrid &g = out.qbox;
-        for (size_t c = 0; c < ncell; ++c)
-            for (uint32_t i = 0; i < out.top; ++i) {
-                const float *f = &cell_boxes[(c * out.top + i) * 6];
-                uint32_t *w = &out.cell_qnodes[(c * out.top + i) * 8];
-                uint32_t q[6];
-                for (int k = 0; k < 3; ++k) {
-                    q[k] = q_down(f[k], g.step[k], g.base[k]);
-                    q[3 + k] = q_up(f[3 + k], g.step[k], g.base[k]);
-                }
-                w[0] = q[0] | q[1] << 16;
-                w[1] = q[2] | q[3] << 16;
-                w[2] = q[4] | q[5] << 16;
-                for (int k = 3; k < 8; ++k) w[k] = out.qnodes[(size_t)i * 8 + k];
-            }
-    }
+    quantize_boxes(out.nodes, 16, true, out.miss, out.qnodes, out.qbox, &out.nbase, &out.nstep);
     return out;
 }
 

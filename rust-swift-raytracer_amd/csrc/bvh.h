@@ -75,20 +75,6 @@ struct TriangleBVH {
     std::vector<uint32_t> qnodes;
     QuantGrid qbox;
     float nbase = -1, nstep = 1;    // normal grid (all three axes)
-    // Per-cell top levels.  Secondary rays start on the
-    // scene's surfaces, far from oc, where the widening of the top levels'
-    // boxes is widest.  Nodes [0, top) are the tree's top levels (breadth-first
-    // order; every node below them keeps the builder order), and each cell of
-    // a grid over the triangles' bounding box holds its own kernel records of
-    // those nodes: boxes of the phantoms for the cell's centre, the same normal
-    // boxes, children and links.  A ray whose origin lies in a cell walks the
-    // top levels through that cell's records, widened from the centre instead
-    // of oc.  Any cell would be exact; the nearest one is the tightest.
-    uint32_t top = 0;               // nodes with per-cell records (0: no cells)
-    float cell_lo[3] = {0, 0, 0};   // grid corner; cell (i, j, k) is centred at
-    float cell_size = 0;            //   cell_lo + ((float)i + 0.5f) * cell_size (float ops)
-    uint32_t cell_dim[3] = {0, 0, 0};
-    std::vector<uint32_t> cell_qnodes;  // (cell (i * dy + j) * dz + k) x top x 8 u32, static grid
 };
 
 // tri_hot: PackedScene::tri_hot (the exact per-triangle n and n.v0 bits).

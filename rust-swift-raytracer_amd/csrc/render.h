@@ -110,13 +110,6 @@ struct TraceParams {
     float tbvh_oc[3];         // origin the boxes were built for (widening uses o - oc)
     float tq_base[3], tq_step[3], tq_nbase, tq_nstep;  // static-tree grids
     float cq_base[3], cq_step[3];                      // camera-tree grid
-    // per-cell top levels of the static tree (bvh.h TriangleBVH::top): nodes
-    // [0, tcell_top) of a ray whose origin lies in cell c are read from
-    // tcells[(c * tcell_top + node) * 2] and widened from the cell's centre
-    const uint4 *tcells;
-    uint32_t tcell_top;       // 0: no cells
-    float tcell_lo[3], tcell_size, tcell_inv;
-    uint32_t tcell_dim[3];
     // the same triangles' phantoms for the camera origin (bvh.h CameraTriangleBVH),
     // used at bounce 0; cam_nnodes == 0: bounce 0 uses the tree above
     const uint4 *cam_nodes;   // 2 per node: quantised box, a, link

@@ -446,20 +446,16 @@ __device__ __forceinline__ bool tri_begin(const TraceParams &p, F3 org, F3 dir, 
 
 // One node of the triangle tree (static or camera-origin); an entered leaf is
 // handed back in `leaf` as (first << 3) | count, like sphere_node.
-// dlt2c, cbase, ctop: the ray's cell (tri_cell): nodes below ctop are read
-// from the cell's records at cbase and widened from its centre
-__device__ __forceinline__ bool tri_node(const TraceParams &p, F3 nlo, F3 nhi, F3 inv, F3 dlt2, F3 dlt2c,
-                                         uint32_t cbase, uint32_t ctop, bool cam, float cap,
-                                         uint32_t &node, uint32_t &leaf, uint32_t &node_tests) {
+__device__ __forceinline__ bool tri_node(const TraceParams &p, F3 nlo, F3 nhi, F3 inv, F3 dlt2, bool cam,
+                                         float cap, uint32_t &node, uint32_t &leaf,
+                                         uint32_t &node_tests) {
     ++node_tests;
     // Quantised nodes (bvh.h QuantGrid): u16 coordinates decoded with one fma
     // on the tree's grid; the host rounds every face outward *after* this
     // exact decode, so a decoded box contains the float box.
     // one 32-B sector per node: (static) box | normals | a | link,
     // (camera) box | a | link; fixed child-a-first order (bvh.cpp)
-    const bool top = node < ctop;
-    const uint4 *qn = cam ? p.cam_nodes + 2u * node : top ? p.tcells + 2u * (cbase + node) : p.tbvh_nodes + 2u * node;
-    const F3 dd = top ? dlt2c : dlt2;
+    const uint4 *qn = (cam ? p.cam_nodes : p.tbvh_nodes) + 2u * node;
     const uint4 q0 = qn[0], q1 = qn[1];
     const uint32_t a = cam ? q0.w : q1.z;
     const uint32_t miss = cam ? q1.x : q1.w;
@@ -484,9 +480,9 @@ __device__ __forceinline__ bool tri_node(const TraceParams &p, F3 nlo, F3 nhi, F
                                   __builtin_fmaf(hi16(q1.y), ns, nb), 0.0f);
     // 2s = n^.(2d) over the normal box, d = o - oc (the tree's box origin,
     // bvh.h); dlt2 = 2d is exact, so 2s m below has the bits of 2 (s m)
-    const float ax = N0.x * dd.x, bx = N1.x * dd.x;
-    const float ay = N0.y * dd.y, by = N1.y * dd.y;
-    const float az = N0.z * dd.z, bz = N1.z * dd.z;
+    const float ax = N0.x * dlt2.x, bx = N1.x * dlt2.x;
+    const float ay = N0.y * dlt2.y, by = N1.y * dlt2.y;
+    const float az = N0.z * dlt2.z, bz = N1.z * dlt2.z;
     const float sl = (fminf(ax, bx) + fminf(ay, by)) + fminf(az, bz);
     const float sh = (fmaxf(ax, bx) + fmaxf(ay, by)) + fmaxf(az, bz);
     // phantom offset 2 s m_k over 2s in [sl, sh], m_k in [N0.k, N1.k]
@@ -517,32 +513,6 @@ __device__ __forceinline__ bool tri_node(const TraceParams &p, F3 nlo, F3 nhi, F
     node = (skip || is_leaf) ? miss : child;
     leaf = a & ~kLeafBitDev;  // read only when the flag is set
     return !skip && is_leaf;
-}
-
-// The ray's cell for the static tree's top levels (bvh.h TriangleBVH::top):
-// any cell is exact (its boxes hold the phantoms for its centre c, widened by
-// the ray from c), the one holding the origin is the tightest.  Origins
-// outside the grid (and camera-tree lanes) get ctop = 0: static records only.
-// The centre is computed with the host's float operations (bvh.cpp).
-__device__ __forceinline__ void tri_cell(const TraceParams &p, F3 org, bool cam, F3 &dlt2c, uint32_t &cbase,
-                                         uint32_t &ctop) {
-    ctop = 0;
-    cbase = 0;
-    dlt2c = f3(0.0f, 0.0f, 0.0f);
-    if (cam || p.tcell_top == 0) return;
-    const float fx = floorf((org.x - p.tcell_lo[0]) * p.tcell_inv);
-    const float fy = floorf((org.y - p.tcell_lo[1]) * p.tcell_inv);
-    const float fz = floorf((org.z - p.tcell_lo[2]) * p.tcell_inv);
-    if (!(fx >= 0.0f && fx < (float)p.tcell_dim[0] && fy >= 0.0f && fy < (float)p.tcell_dim[1] &&
-          fz >= 0.0f && fz < (float)p.tcell_dim[2]))
-        return;
-    const uint32_t ix = (uint32_t)fx, iy = (uint32_t)fy, iz = (uint32_t)fz;
-    const float cx = p.tcell_lo[0] + ((float)ix + 0.5f) * p.tcell_size;
-    const float cy = p.tcell_lo[1] + ((float)iy + 0.5f) * p.tcell_size;
-    const float cz = p.tcell_lo[2] + ((float)iz + 0.5f) * p.tcell_size;
-    dlt2c = f3(2.0f * (org.x - cx), 2.0f * (org.y - cy), 2.0f * (org.z - cz));
-    cbase = ((ix * p.tcell_dim[1] + iy) * p.tcell_dim[2] + iz) * p.tcell_top;
-    ctop = p.tcell_top;
 }
 
 __device__ __forceinline__ void tri_leaf(const TraceParams &p, F3 org, F3 dir, bool cam,
@@ -1005,16 +975,13 @@ void trace_kernel(TraceParams p) {
                 const bool cam = bounce == 0 && p.cam_nnodes != 0;
                 const F3 dlt2 = f3(2.0f * (org.x - p.tbvh_oc[0]), 2.0f * (org.y - p.tbvh_oc[1]),
                                    2.0f * (org.z - p.tbvh_oc[2]));
-                F3 dlt2c;
-                uint32_t cbase, ctop;
-                tri_cell(p, org, cam, dlt2c, cbase, ctop);
                 // rho (e; 0 on the camera tree) folded into the slab offsets
                 F3 nlo, nhi;
                 sphere_slabs(org, inv, e, nlo, nhi);
                 float cap = fminf(best_t, tri_t);
                 do {
                     uint32_t leaf;
-                    if (tri_node(p, nlo, nhi, inv, dlt2, dlt2c, cbase, ctop, cam, cap, node, leaf, tnode_tests)) {
+                    if (tri_node(p, nlo, nhi, inv, dlt2, cam, cap, node, leaf, tnode_tests)) {
                         tri_leaf(p, org, dir, cam, leaf, best_t, tri_t, tri_i, tri_in, tri_done);
                         cap = fminf(best_t, tri_t);
                     }

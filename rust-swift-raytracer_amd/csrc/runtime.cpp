@@ -51,7 +51,7 @@ DeviceState::~DeviceState() {
     if (hipSetDevice(device) != hipSuccess) return;
     void *bufs[] = {sph_hot, sph_cold, tri_hot, tri_geo, mats, samples, ring, out, replay, counter, stats,
                     bvh_nodes, bvh_prims, big_hot, bvh_miss, bvh_prim_id, big_id, bvh_miss16,
-                    sph_shade, sph_kind, tbvh_nodes, tcells, tbvh_tris, tbvh_loose,
+                    sph_shade, sph_kind, tbvh_nodes, tbvh_tris, tbvh_loose,
                     cam_nodes, cam_tris, ptl_off, ptl_items, spl, tile, gath,
                     sstates, stab, sscan, sclaim, swin, sjump, sctrl, sbend, spath, sfin,
                     gspl, gspl_rects, gspl_flag, scheck};
@@ -179,7 +179,6 @@ static int device_for(WorldState &w, int want, DeviceState *&out) {
                 return hipMemcpy(*dst, src.data(), src.size() * sizeof(uint32_t), hipMemcpyHostToDevice);
             };
             HIP_TRY(upu((void **)&d->tbvh_nodes, tb.qnodes));
-            if (tb.top) HIP_TRY(upu((void **)&d->tcells, tb.cell_qnodes));
             HIP_TRY(up((void **)&d->tbvh_tris, tb.tris));
             HIP_TRY(upu((void **)&d->tbvh_loose, tb.loose));
             d->tnodes = (uint32_t)(tb.qnodes.size() / 8);
@@ -532,16 +531,6 @@ int render_frame(WorldState &w, const CameraModel &cam, size_t width, size_t hei
         }
         p.tq_nbase = tb.nbase;
         p.tq_nstep = tb.nstep;
-        if (d->tcells && env_u64("RT_AMD_TRI_CELL_USE", 1) != 0) {
-            p.tcells = d->tcells;
-            p.tcell_top = tb.top;
-            for (int k = 0; k < 3; ++k) {
-                p.tcell_lo[k] = tb.cell_lo[k];
-                p.tcell_dim[k] = tb.cell_dim[k];
-            }
-            p.tcell_size = tb.cell_size;
-            p.tcell_inv = 1.0f / tb.cell_size;
-        }
         p.tbvh_r = tb.radius; p.tbvh_mag = tb.mag;
     }
     const float inv_spp = 1.0f / (float)o.samples_per_pixel;  // 1.0 / spp as f32 (common.rs:345)

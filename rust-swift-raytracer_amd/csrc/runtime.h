@@ -40,7 +40,6 @@ struct DeviceState {
     uint16_t *bvh_miss16 = nullptr;
     uint32_t nnodes = 0, nbig = 0, nprims = 0;
     uint4 *tbvh_nodes = nullptr;                                // triangle BVH (bvh.h qnodes)
-    uint4 *tcells = nullptr;                                    // its per-cell top levels
     float4 *tbvh_tris = nullptr;
     uint32_t *tbvh_loose = nullptr;
     uint32_t tnodes = 0, ttris = 0, tloose = 0;

@@ -108,62 +108,6 @@ static void check_quant(const std::vector<float> &nodes, size_t stride, const st
     }
 }
 
-// Per-cell top levels (bvh.h TriangleBVH::top): the top nodes are a
-// breadth-first prefix (parents before children, siblings adjacent); each
-// cell record carries the static record's normal box, child word and link;
-// and its decoded box holds every vertex of the node's triangles moved to
-// their phantom for the cell's centre, v + 2(n^.c)n^ (n^ from the record's n).
-static void check_cells(const TriangleBVH &t) {
-    if (!t.top) return;
-    const size_t n = t.nodes.size() / 16, top = t.top;
-    const size_t ncell = (size_t)t.cell_dim[0] * t.cell_dim[1] * t.cell_dim[2];
-    CHECK(t.cell_qnodes.size() == ncell * top * 8, "cells: %zu words for %zu cells\n", t.cell_qnodes.size(), ncell);
-    if (t.cell_qnodes.size() != ncell * top * 8) return;
-    std::vector<uint32_t> first(n), count(n);
-    for (size_t i = n; i-- > 0;) {
-        const uint32_t a = bits(t.nodes[i * 16 + 3]);
-        if (a & kLeafBit) { first[i] = a & ~kLeafBit; count[i] = bits(t.nodes[i * 16 + 7]); continue; }
-        CHECK(a > i, "cells: child %u before parent %zu\n", a, i);
-        if (a <= i) return;
-        first[i] = first[a];
-        count[i] = count[a] + count[a + 1];
-        if (i >= top) CHECK(a >= top, "cells: node %zu below the top levels has a top child\n", i);
-    }
-    auto dec = [](uint32_t v, float s, float b) { return std::fmaf((float)v, s, b); };
-    for (size_t c = 0; c < ncell; ++c) {
-        const uint32_t ci = (uint32_t)(c / ((size_t)t.cell_dim[1] * t.cell_dim[2]));
-        const uint32_t cj = (uint32_t)(c / t.cell_dim[2] % t.cell_dim[1]);
-        const uint32_t ck = (uint32_t)(c % t.cell_dim[2]);
-        const double cc[3] = {t.cell_lo[0] + ((float)ci + 0.5f) * t.cell_size,
-                              t.cell_lo[1] + ((float)cj + 0.5f) * t.cell_size,
-                              t.cell_lo[2] + ((float)ck + 0.5f) * t.cell_size};
-        for (size_t i = 0; i < top; ++i) {
-            const uint32_t *w = &t.cell_qnodes[(c * top + i) * 8];
-            for (int k = 3; k < 8; ++k)
-                CHECK(w[k] == t.qnodes[i * 8 + k], "cells: cell %zu node %zu word %d differs\n", c, i, k);
-            const uint32_t u[6] = {w[0] & 0xFFFF, w[0] >> 16, w[1] & 0xFFFF, w[1] >> 16, w[2] & 0xFFFF, w[2] >> 16};
-            double lo[3], hi[3];
-            for (int k = 0; k < 3; ++k) {
-                lo[k] = dec(u[k], t.qbox.step[k], t.qbox.base[k]);
-                hi[k] = dec(u[3 + k], t.qbox.step[k], t.qbox.base[k]);
-            }
-            for (uint32_t j = first[i]; j < first[i] + count[i]; ++j) {
-                const float *r = &t.tris[(size_t)j * 16];
-                const double nn = std::sqrt((double)r[0] * r[0] + (double)r[1] * r[1] + (double)r[2] * r[2]);
-                const double nh[3] = {r[0] / nn, r[1] / nn, r[2] / nn};
-                const double s = nh[0] * cc[0] + nh[1] * cc[1] + nh[2] * cc[2];
-                for (int v = 1; v <= 3; ++v)
-                    for (int k = 0; k < 3; ++k) {
-                        const double x = (double)r[4 * v + k] + 2 * s * nh[k];
-                        CHECK(x >= lo[k] - 1e-9 * (1 + std::fabs(x)) && x <= hi[k] + 1e-9 * (1 + std::fabs(x)),
-                              "cells: cell %zu node %zu misses a phantom vertex (axis %d: %g not in [%g, %g])\n",
-                              c, i, k, x, lo[k], hi[k]);
-                    }
-            }
-        }
-    }
-}
-
 int main(int argc, char **argv) {
     std::ifstream fh(argv[1]);
     std::stringstream ss;
@@ -183,7 +127,6 @@ int main(int argc, char **argv) {
         check_tree(tb.nodes, 16, tb.tris.size() / 16, leaf, "static");
         check_links(tb.nodes, 16, tb.miss, "static");
         check_quant(tb.nodes, 16, tb.qnodes, tb.miss, tb.qbox, tb.nbase, tb.nstep, "static");
-        check_cells(tb);
         const float o[3] = {s.camera.origin.x, s.camera.origin.y, s.camera.origin.z};
         cb = build_camera_triangle_bvh(s.triangles, p.tri_hot, tb, o, leaf);
         check_tree(cb.nodes, 8, cb.tris.size() / 16, leaf, "camera");
@@ -203,9 +146,8 @@ int main(int argc, char **argv) {
               "triangles lost: %zu tree + %zu loose + %zu degenerate < %zu\n", in_tree, tb.loose.size(),
               degenerate, s.triangles.size());
     if (fails) return 1;
-    std::printf("OK spheres %zu nodes %zu | triangles %zu tree %zu loose %zu nodes %zu camera nodes %zu"
-                " | cells %u x %u x %u top %u\n",
+    std::printf("OK spheres %zu nodes %zu | triangles %zu tree %zu loose %zu nodes %zu camera nodes %zu\n",
                 s.spheres.size(), sb.nodes.size() / 8, s.triangles.size(), in_tree, tb.loose.size(),
-                tb.nodes.size() / 16, cb.nodes.size() / 8, tb.cell_dim[0], tb.cell_dim[1], tb.cell_dim[2], tb.top);
+                tb.nodes.size() / 16, cb.nodes.size() / 8);
     return 0;
 }
