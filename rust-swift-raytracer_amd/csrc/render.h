@@ -137,18 +137,6 @@ struct TraceParams {
     uint32_t sspp;            // the frame's spp ...
     FastDiv div_sspp;         // ... and its divider
     uint32_t max_draws;       // 2 + 3 * max(depth, 0): bound of the draw count search
-    // kRngSerialCount chain mode (chain_mask != 0): the pool holds only the
-    // candidates of every (chain_mask + 1)-th sample; a lane that finishes
-    // candidate (jl, B) continues with (jl + 1, B + b) -- the one entry of the
-    // next sample the true path could take from there -- unless that entry is
-    // outside the window, starts a new run, or was claimed already (claim[]:
-    // one u32 per table entry, claimed by raising it to `tag`, the iteration's
-    // number).  Only the entries some path from a run's first sample reaches
-    // are traced; the walks read no others.
-    uint32_t *claim;
-    uint32_t chain_mask;      // run length - 1 (a power of two), 0 = every candidate
-    uint32_t nlaunch;         // chain mode: samples of the launch (p.npix = runs)
-    uint32_t tag;             // (set in the kernel: ctrl[7] + ctrl[3] + 1; ctrl[7] = 0)
 };
 
 // Candidate k of chunk sample jl (frame sample a + jl) means B = serial_lo + k

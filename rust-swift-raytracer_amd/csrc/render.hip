@@ -552,17 +552,13 @@ __device__ __forceinline__ void job_pixel(const TraceParams &p, uint32_t job, ui
     row = p.height - 1u - ir;
 }
 
-// kRngSerialCount: the offset B (scatters since the iteration's first sample)
-// of job = launch sample jl * K + candidate k
-__device__ __forceinline__ uint32_t serial_offset(const TraceParams &p, uint32_t jl, uint32_t k) {
-    return serial_lo(p.sM, p.cbase, jl, p.spp, (p.max_draws - 2u) / 3u, p.nserial) + k;
-}
-
 // SERIAL passes: the start state of job (launch sample jl, variant k).
 __device__ __forceinline__ uint32_t serial_start(const TraceParams &p, uint32_t job) {
     const uint32_t jl = fdiv(job, p.div_spp);
     const uint32_t k = job - jl * p.spp;
-    if (p.mode == kRngSerialCount) return p.win[2u * jl + 3u * serial_offset(p, jl, k)];
+    if (p.mode == kRngSerialCount)
+        return p.win[2u * jl + 3u * (serial_lo(p.sM, p.cbase, jl, p.spp, (p.max_draws - 2u) / 3u,
+                                               p.nserial) + k)];
     if (p.mode == kRngSerialCheck) return p.win[p.cbase + jl];
     return counter_seed(p.seed, (uint64_t)(p.cbase + jl) * p.spp + k);
 }
@@ -710,15 +706,13 @@ void trace_kernel(TraceParams p) {
         p.cbase = p.ctrl[4];  // (the walks advance it)
         const uint32_t K = p.ctrl[5];
         if (p.mode == kRngSerialCount && K != 0u && K < p.spp) {
-            if (p.chain_mask == 0u) p.chunk = (p.chunk / K) * K;  // (whole samples, ~ as many jobs per atomic)
+            // (chunks of whole samples stay whole samples, about as many jobs per atomic)
+            if (p.chunk % p.spp == 0u) p.chunk = (p.chunk / K) * K;
             p.spp = K;
             p.div_spp = make_fastdiv(K);
             p.njobs = p.npix * K;
         }
-        p.tag = p.ctrl[7] + p.ctrl[3] + 1u;
     }
-    // chain mode: a lane's next (sample, candidate) job, ~0u = none
-    uint32_t cont = ~0u;
     const uint32_t lane = __lane_id();
     extern __shared__ float4 lds[];
     BvhView view;
@@ -1089,21 +1083,6 @@ void trace_kernel(TraceParams p) {
                         ++n;
                     }
                     out_r = (x == rng && n >= 2u) ? (float)((n - 2u) / 3u) : -1.0f;
-                    if (p.chain_mask != 0u && p.mode == kRngSerialCount && out_r >= 0.0f) {
-                        // chain mode: the path from this entry goes on at (jl + 1,
-                        // B + b) -- traced by this lane unless another one got there
-                        // first (then both paths are one from here on)
-                        const uint32_t jl = fdiv(slot, p.div_spp);
-                        const uint32_t j1 = jl + 1u;
-                        if ((j1 & p.chain_mask) != 0u && j1 < p.nlaunch) {
-                            const uint32_t B1 = serial_offset(p, jl, slot - jl * p.spp) + (n - 2u) / 3u;
-                            const uint32_t l1 = serial_offset(p, j1, 0u);
-                            if (B1 >= l1 && B1 - l1 < p.spp) {
-                                const uint32_t e = j1 * p.spp + (B1 - l1);
-                                if (atomicMax(p.claim + e, p.tag) < p.tag) cont = e;
-                            }
-                        }
-                    }
                 }
                 // planar (R, G, B planes): 12 B per sample, to the slab or the
                 // ring (SERIAL passes: plane 0 only)
@@ -1152,13 +1131,8 @@ void trace_kernel(TraceParams p) {
         // ---- refill lanes whose path ended (active-ray compaction) -------
         // (with the fused resolve a new chunk needs a free ring slot: with all
         // kTraceRing slots waiting on unfinished samples the lanes stay idle)
-        // SERIAL chain mode: lanes whose path goes on take their next entry
-        // first, whatever the pool's state; the others take pool jobs
-        const uint64_t contm = kSerial ? __ballot(!active && cont != ~0u) : 0ull;
-        const uint64_t pdead = dead & ~contm;
-        const bool prefill = refill && !exhausted && !(fused && rfree == 0 && pool_next >= pool_end);
-        if (prefill || contm != 0ull) {
-            if (prefill && pool_next >= pool_end) {
+        if (refill && !exhausted && !(fused && rfree == 0 && pool_next >= pool_end)) {
+            if (pool_next >= pool_end) {
                 uint32_t base = 0;
                 if (lane == 0) {
                     base = pbegin + (prefetch_pending ? prefetch
@@ -1198,22 +1172,11 @@ void trace_kernel(TraceParams p) {
                     }
                 }
             }
-            const uint32_t avail = prefill ? pool_end - pool_next : 0u;
+            const uint32_t avail = pool_end - pool_next;
             const uint32_t rank = __builtin_amdgcn_mbcnt_hi(
-                (uint32_t)(pdead >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)pdead, 0u));
-            const bool own = kSerial && cont != ~0u;  // (only !active lanes hold one)
-            if (own || (!active && rank < avail)) {
-                uint32_t job = pool_next + rank;
-                if (kSerial) {
-                    if (own) {
-                        job = cont;
-                        cont = ~0u;
-                    } else if (p.chain_mask != 0u) {
-                        // pool job q = run r's candidate k -> job of sample r * run
-                        const uint32_t r = fdiv(job, p.div_spp);
-                        job = r * ((p.chain_mask + 1u) * p.spp) + (job - r * p.spp);
-                    }
-                }
+                (uint32_t)(dead >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)dead, 0u));
+            if (!active && rank < avail) {
+                const uint32_t job = pool_next + rank;
                 // Jobs are enumerated pixel-major (job = pixel*spp + s): the
                 // lanes refilled together trace samples of one pixel (or of
                 // neighbours), so their primary walks visit the same nodes
@@ -1265,10 +1228,10 @@ void trace_kernel(TraceParams p) {
                 phase = kSetup;
                 active = true;
             }
-            pool_next += min((uint32_t)__popcll(pdead), avail);
+            pool_next += min(ndead, avail);
             // ask for the next chunk now; the reply is only waited for when the
             // pool runs dry (hides the ~1-3 us atomic round trip)
-            if (prefill && !exhausted && !prefetch_pending && pool_end - pool_next < kWave) {
+            if (!exhausted && !prefetch_pending && pool_end - pool_next < kWave) {
                 if (lane == 0) prefetch = atomicAdd(p.job_counter + 32u * part, p.chunk);
                 prefetch_pending = true;
             }

@@ -53,7 +53,7 @@ DeviceState::~DeviceState() {
                     bvh_nodes, bvh_prims, big_hot, bvh_miss, bvh_prim_id, big_id, bvh_miss16,
                     sph_shade, sph_kind, tbvh_nodes, tbvh_tris, tbvh_loose,
                     cam_nodes, cam_tris, ptl_off, ptl_items, spl, tile, gath,
-                    sstates, stab, sscan, sclaim, swin, sjump, sctrl, sbend, spath, sfin,
+                    sstates, stab, sscan, swin, sjump, sctrl, sbend, spath, sfin,
                     gspl, gspl_rects, gspl_flag, scheck};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
@@ -575,13 +575,10 @@ int render_frame(WorldState &w, const CameraModel &cam, size_t width, size_t hei
     if (sp) {
         // one SERIAL pass: nsamples x variants jobs (job = launch sample *
         // variants + variant); each stores its scatter count to slab plane 0
-        const uint64_t ntab = (uint64_t)sp->nsamples * sp->variants;  // table entries
-        const bool chain = sp->mode == kRngSerialCount && sp->chain > 1 && sp->claim != nullptr;
-        const uint64_t nruns = chain ? ((uint64_t)sp->nsamples + sp->chain - 1) / sp->chain : sp->nsamples;
-        const uint64_t njobs = nruns * sp->variants;  // pool jobs
+        const uint64_t njobs = (uint64_t)sp->nsamples * sp->variants;
         if (njobs == 0) return 0;
-        if (ntab > 0x7FFFFFFFull) { set_error("serial pass too large"); return -1; }
-        HIP_TRY(grow(d->samples, d->samples_cap, 3 * ntab));
+        if (njobs > 0x7FFFFFFFull) { set_error("serial pass too large"); return -1; }
+        HIP_TRY(grow(d->samples, d->samples_cap, 3 * njobs));
         p.samples = d->samples;
         p.ring = nullptr;
         p.ring_shift = 0;
@@ -597,26 +594,22 @@ int render_frame(WorldState &w, const CameraModel &cam, size_t width, size_t hei
         p.ctrl = sp->ctrl;
         p.max_draws = 2u + 3u * (uint32_t)std::max(o.max_ray_bounces, 0);
         p.njobs = (uint32_t)njobs;
-        p.npix = (uint32_t)nruns;
-        p.nlaunch = sp->nsamples;
-        p.chain_mask = chain ? sp->chain - 1u : 0u;
-        p.claim = chain ? sp->claim : nullptr;
-        // chain mode: a lane whose path goes on is re-initialised at once
-        if (chain) p.refill_min = 1;
+        p.npix = sp->nsamples;
         p.slab_row0 = 0;
         const uint64_t jobs_per_block = waves_per_block * 256;
-        // (chain mode: each pool job starts a run of up to `chain` samples)
         const uint64_t blocks = std::max<uint64_t>(
-            1, std::min<uint64_t>(full_blocks, (ntab + jobs_per_block - 1) / jobs_per_block));
+            1, std::min<uint64_t>(full_blocks, (njobs + jobs_per_block - 1) / jobs_per_block));
         const uint64_t nwaves = blocks * waves_per_block;
+        // the count pass: chunks of 128 jobs, not whole samples of K candidates
+        // (the end of the launch drains sooner: c_raytracer 960x540x16 SERIAL
+        // 671 -> 608 ms; 64: 610 ms; more partitions cost, 64: +8 %, 256: +30 %)
         uint64_t chunk = std::min<uint64_t>(256, std::max<uint64_t>(64, njobs / (nwaves * 16) / 64 * 64));
         chunk = chunk >= sp->variants ? chunk / sp->variants * sp->variants : sp->variants;
-        // chain mode: a pool job starts a run of up to `chain` samples, so the
-        // runs are spread thin (a few per lane), not one sample's K per wave
-        if (chain) chunk = std::max<uint64_t>(1, std::min<uint64_t>(64, njobs / (nwaves * 4)));
-        p.chunk = (uint32_t)chunk;
-        const uint64_t parts = std::max<uint64_t>(
+        if (sp->mode == kRngSerialCount) chunk = env_u64("RT_AMD_SERIAL_CCHUNK", 128);
+        p.chunk = (uint32_t)std::max<uint64_t>(1, chunk);
+        uint64_t parts = std::max<uint64_t>(
             1, std::min<uint64_t>({(uint64_t)(p.step ? 64 : 16), kMaxParts, njobs / (16 * chunk) + 1}));
+        if (const uint64_t np = env_u64("RT_AMD_SERIAL_PARTS", 0)) parts = std::min<uint64_t>(np, kMaxParts);
         p.nparts = (uint32_t)parts;
         HIP_TRY(hipMemsetAsync(d->counter, 0, parts * 128, s));
         HIP_TRY(launch_trace(p, (uint32_t)blocks, s));
@@ -918,17 +911,6 @@ static int serial_find_states(WorldState &w, const CameraModel &cam, size_t widt
             HIP_TRY(hipMemcpy(d->sjump, jt.data(), jt.size() * 4, hipMemcpyHostToDevice));
         }
         if (!d->sctrl) HIP_TRY(hipMalloc((void **)&d->sctrl, 32));
-        // chain mode (render.h TraceParams::claim): runs of `chain` samples, a
-        // power of two dividing the walk's block of R_walk samples, so every
-        // block starts a run (the walks start there from every candidate)
-        uint32_t chain = (uint32_t)std::min<uint64_t>(env_u64("RT_AMD_SERIAL_RUN", 1), 1u << 20);
-        while (chain > 1 && ((chain & (chain - 1)) != 0 || R_walk % chain != 0)) --chain;
-        if (chain > 1) {
-            // tags: iteration i claims with i + 1 (render.h TraceParams::tag),
-            // on a table zeroed for each frame
-            HIP_TRY(grow(d->sclaim, d->sclaim_cap, L * K));
-            HIP_TRY(hipMemsetAsync(d->sclaim, 0, L * K * 4, s));
-        }
         const uint32_t ctrl0[8] = {0u, o.seed, 0u, 0u, 0u, K0, 0u, 0u};  // Random::new() (random.rs:8-10)
         HIP_TRY(hipMemcpyAsync(d->sctrl, ctrl0, 32, hipMemcpyHostToDevice, s));
         // iterations are queued in batches sized by the expected progress;
@@ -953,7 +935,7 @@ static int serial_find_states(WorldState &w, const CameraModel &cam, size_t widt
             for (uint64_t q = 0; q < it; ++q) {
                 HIP_TRY(launch_serial_window(d->sctrl, d->sjump, d->swin, (uint32_t)wlen, s));
                 const SerialPass sp{kRngSerialCount, 0u, (uint32_t)L, (uint32_t)K, d->swin, pred,
-                                    d->sctrl, chain, chain > 1 ? d->sclaim : nullptr};
+                                    d->sctrl};
                 rc = render_frame(w, cam, width, height, ob, nullptr, s, nullptr, &sp);
                 if (rc) return rc;
                 HIP_TRY(launch_serial_walk(d->sctrl, d->samples, pred, adapt ? Vdev : nullptr,

@@ -78,7 +78,6 @@ struct DeviceState {
     uint32_t *sfin = nullptr;                               // chain result (4 + 256)
     uint32_t *sjump = nullptr;
     uint32_t *sctrl = nullptr;
-    uint32_t *sclaim = nullptr;      size_t sclaim_cap = 0;  // chain-mode claims (tagged)
     unsigned long long *scheck = nullptr;                       // chain-check count
     uint32_t *counter = nullptr;                                // job counter
     unsigned long long *stats = nullptr; size_t stats_cap = 0;  // per-wave counter records
@@ -130,8 +129,6 @@ struct SerialPass {
     const uint32_t *win;
     SerialPred M;
     const uint32_t *ctrl;
-    uint32_t chain = 0;       // kRngSerialCount: run length (power of two), 0/1 = every candidate
-    uint32_t *claim = nullptr;  // chain mode: nsamples * variants u32 (TraceParams::claim)
 };
 
 // Renders rank's tile of a width x height frame into device memory d_out

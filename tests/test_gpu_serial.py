@@ -70,7 +70,9 @@ def test_serial_narrow_windows_and_short_iterations(monkeypatch):
     windows after a few samples and each iteration resumes where the last one
     stopped; one-sample iterations; iterations longer than the frame; one K
     for every iteration (no per-iteration windows from the pixel variances);
-    states re-walked per block instead of gathered from the recorded paths."""
+    states re-walked per block instead of gathered from the recorded paths;
+    odd iteration lengths with shallow paths; count-pass chunks and
+    partitions of any size."""
     for env, scene, size in [
         (dict(RT_AMD_SERIAL_K="24", RT_AMD_SERIAL_CHUNK="512"), "c_raytracer_world.txt", (80, 60, 16, 8)),
         (dict(RT_AMD_SERIAL_ADAPT="0"), "c_raytracer_world.txt", (40, 30, 16, 8)),
@@ -82,6 +84,11 @@ def test_serial_narrow_windows_and_short_iterations(monkeypatch):
         (dict(RT_AMD_SERIAL_CHUNK="1"), "world.txt", (12, 9, 2, 8)),
         (dict(RT_AMD_SERIAL_CHUNK="100"), "world.txt", (13, 7, 3, 8)),
         (dict(RT_AMD_SERIAL_CHUNK="100000", RT_AMD_SERIAL_Z10="5"), "world.txt", (31, 17, 4, 8)),
+        # odd iteration lengths, shallow paths
+        (dict(RT_AMD_SERIAL_CHUNK="37"), "world.txt", (15, 9, 3, 1)),
+        (dict(RT_AMD_SERIAL_CHUNK="61", RT_AMD_SERIAL_K="4"), "world.txt", (15, 9, 3, 1)),
+        # count-pass scheduling: small chunks of any size, many partitions
+        (dict(RT_AMD_SERIAL_CCHUNK="37", RT_AMD_SERIAL_PARTS="256"), "c_raytracer_world.txt", (40, 30, 16, 8)),
     ]:
         for k, v in env.items():
             monkeypatch.setenv(k, v)
