@@ -13,6 +13,8 @@
 //                     cell centre, widened per ray from it) for depth < D
 //   SIM_HYB_RANGE=1   ... boxes over the whole cell instead (no widening)
 //   SIM_LEVELS=1      share of visits per tree level
+//   SIM_BIN=P         secondary rays of P-ray pools, waves in arrival order vs
+//                     binned by octant + origin cell (SIM_BIN_KEY, SIM_BIN_CELL)
 //   SIM_Q8=B,N        16-B nodes in DFS preorder: N>0 u8 boxes and normal boxes
 //                     on per-block frames (B nodes per block; N=3 per-axis
 //                     normal frames), N=0 u16 boxes with one normal box per
@@ -514,6 +516,84 @@ int main(int argc, char **argv) {
                     "walk %.0f, lockstep distinct nodes %.0f, union %.0f (non-monotone steps %.0f)\n",
                     G, cosine ? "+z diffuse" : "uniform", groups, lanes / groups, maxl / groups, uniq / groups,
                     uni / groups, nonmono);
+        return 0;
+    }
+    if (const char *bs = std::getenv("SIM_BIN")) {
+        // Secondary-ray binning: pools of P rays (P/16 consecutive pixels x 16
+        // samples, as a workgroup's lanes would hold them), cut into waves of 64
+        // either in arrival order (4 pixels per wave) or after sorting the pool
+        // by direction octant then origin (SIM_BIN_KEY=1: octant only, 2:
+        // octant + 8-unit... origin cell of SIM_BIN_CELL units).  Per wave: lane
+        // visits, the longest walk, the lockstep distinct nodes (L2 requests of
+        // independent walks) and the union (a packet walk's scalar loads).
+        const int P = std::max(64, std::atoi(bs)) / 64 * 64;
+        const int key = std::getenv("SIM_BIN_KEY") ? std::atoi(std::getenv("SIM_BIN_KEY")) : 2;
+        const float cell = std::getenv("SIM_BIN_CELL") ? (float)std::atof(std::getenv("SIM_BIN_CELL")) : 1.0f;
+        uint32_t rng3 = 12345u;
+        auto rnd3 = [&]() { rng3 ^= rng3 << 13; rng3 ^= rng3 >> 17; rng3 ^= rng3 << 5; return rng3 * 0x1p-32f; };
+        struct R { uint64_t k; std::vector<uint32_t> w; };
+        double st[2][4] = {};
+        double waves = 0;
+        const int ppool = P / 16;
+        Count wc, dummy;
+        for (int pix0 = 0; pix0 + ppool <= W * H; pix0 += ppool) {
+            std::vector<R> pool;
+            for (int q = 0; q < ppool; ++q) {
+                const int i = (pix0 + q) % W, j = (pix0 + q) / W;
+                for (int k = 0; k < 16; ++k) {
+                    const float u = (i + rnd3()) / W, v = (j + rnd3()) / H;
+                    V d = unit(sub(add(add(V{cm.lower_left.x, cm.lower_left.y, cm.lower_left.z},
+                                           mul(V{cm.horizontal.x, cm.horizontal.y, cm.horizontal.z}, u)),
+                                       mul(V{cm.vertical.x, cm.vertical.y, cm.vertical.z}, v)), org));
+                    const float tt = trace(t, org, d, dummy);
+                    V o2 = org, d2 = d;
+                    R r;
+                    if (std::isfinite(tt)) {
+                        o2 = add(org, mul(d, tt));
+                        d2 = unit(V{rnd3() * 2 - 1, rnd3() * 2 - 1, rnd3() * 2 - 1});
+                        g_visits = &r.w;
+                        trace(t, o2, d2, wc);
+                        g_visits = nullptr;
+                    }
+                    const uint64_t oct = (d2.x < 0) | ((d2.y < 0) << 1) | ((d2.z < 0) << 2);
+                    auto cq = [&](float x) { return (uint64_t)(int64_t)std::floor(x / cell + 512) & 1023u; };
+                    r.k = (oct << 40) | (key >= 2 ? (cq(o2.x) << 20 | cq(o2.y) << 10 | cq(o2.z)) : 0);
+                    pool.push_back(std::move(r));
+                }
+            }
+            for (int mode = 0; mode < 2; ++mode) {
+                std::vector<R *> order;
+                for (auto &r : pool) order.push_back(&r);
+                if (mode == 1)
+                    std::stable_sort(order.begin(), order.end(), [](const R *a, const R *b) { return a->k < b->k; });
+                for (size_t w0 = 0; w0 < order.size(); w0 += 64) {
+                    size_t mx = 0;
+                    double lanes = 0;
+                    std::vector<uint32_t> all;
+                    for (size_t l = w0; l < w0 + 64; ++l) {
+                        mx = std::max(mx, order[l]->w.size());
+                        lanes += order[l]->w.size();
+                        all.insert(all.end(), order[l]->w.begin(), order[l]->w.end());
+                    }
+                    double uq = 0;
+                    for (size_t s2 = 0; s2 < mx; ++s2) {
+                        std::vector<uint32_t> at;
+                        for (size_t l = w0; l < w0 + 64; ++l)
+                            if (s2 < order[l]->w.size()) at.push_back(order[l]->w[s2]);
+                        std::sort(at.begin(), at.end());
+                        uq += std::unique(at.begin(), at.end()) - at.begin();
+                    }
+                    std::sort(all.begin(), all.end());
+                    const double un = (double)(std::unique(all.begin(), all.end()) - all.begin());
+                    st[mode][0] += lanes; st[mode][1] += (double)mx; st[mode][2] += uq; st[mode][3] += un;
+                    if (mode == 0) waves += 1;
+                }
+            }
+        }
+        for (int mode = 0; mode < 2; ++mode)
+            std::printf("pool %d, %s: per wave lane visits %.0f, longest %.0f, lockstep distinct %.0f, union %.0f\n",
+                        P, mode ? "binned" : "arrival order", st[mode][0] / waves, st[mode][1] / waves,
+                        st[mode][2] / waves, st[mode][3] / waves);
         return 0;
     }
     if (const char *hs = std::getenv("SIM_HYB")) {
