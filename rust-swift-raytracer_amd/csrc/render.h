@@ -196,7 +196,8 @@ hipError_t launch_serial_window(const uint32_t *ctrl, const uint32_t *jump, uint
 // the slab) as far as it stays inside the candidate windows (at least one
 // sample), writes those samples' start states to states[a + jl] and advances
 // ctrl (a, the state at a, resolved).  bend: scratch of
-// ceil(L / serial_walk_block(L)) * K u32.
+// ceil(L / serial_walk_block(L)) * K + 4 u32 (the finish kernel's 16-B loads read up to
+// 3 words past the end).
 uint32_t serial_walk_block(uint32_t L);
 // path, fin (optional, both or neither): scratch of ceil(L / R) R K u32 for the
 // block walks' recorded paths and 4 + 256 u32 for the chain's result; with

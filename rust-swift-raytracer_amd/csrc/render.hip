@@ -1468,6 +1468,8 @@ __global__ __launch_bounds__(256) void serial_window_kernel(const uint32_t *__re
 //     start, writing start states (win[2 jl + 3 B]); ctrl advances past the
 //     resolved samples (>= 1: sample a's own window always holds B = 0).
 constexpr uint32_t kWalkInvalid = 0xFFFFFFFFu;
+constexpr uint32_t kWalkLeft = 0x80000000u;  // bend: the walk left a window (offsets stay below 2^31)
+constexpr uint32_t kChainLds = 12288;  // u32 of block-end rows staged per chunk (48 KB)
 __device__ __forceinline__ uint32_t walk_step(const float *table, const SerialPred &M, uint32_t a,
                                               uint32_t K, uint32_t depth, uint32_t nserial, uint32_t jl,
                                               uint32_t B) {
@@ -1500,21 +1502,29 @@ __global__ __launch_bounds__(256) void serial_walk_blocks_kernel(
     const uint32_t j0 = blk * R, j1 = min(j0 + R, n);
     const size_t stride = (size_t)nb * K;
     uint32_t B = serial_lo(M, a, j0, K, depth, nserial) + k0;
-    for (uint32_t jl = j0; jl < j1 && B != kWalkInvalid; ++jl) {
+    uint32_t jl = j0;
+    for (; jl < j1; ++jl) {
         if (path) path[(size_t)(jl - j0) * stride + t] = B;
-        B = walk_step(table, M, a, K, depth, nserial, jl, B);
+        const uint32_t nB = walk_step(table, M, a, K, depth, nserial, jl, B);
+        if (nB == kWalkInvalid) break;
+        B = nB;
     }
-    bend[t] = B;
+    // the block's end offset, or kWalkLeft | the samples whose end was found
+    // (the path then holds the start offset of the sample that left)
+    bend[t] = jl == j1 ? B : kWalkLeft | (jl - j0);
 }
 
 __global__ __launch_bounds__(256) void serial_walk_finish_kernel(
     uint32_t *__restrict__ ctrl, const float *__restrict__ table, SerialPred M,
     const double *__restrict__ V, uint32_t npix, uint32_t spp, const uint32_t *__restrict__ win,
-    const uint32_t *__restrict__ bend, uint32_t *__restrict__ states, uint32_t *__restrict__ fin, uint32_t L,
-    uint32_t Kmax, uint32_t R, uint32_t depth, uint32_t nserial, float z, float sfloor) {
+    const uint32_t *__restrict__ bend, const uint32_t *__restrict__ path, uint32_t *__restrict__ states,
+    uint32_t *__restrict__ fin, uint32_t L, uint32_t Kmax, uint32_t R, uint32_t depth, uint32_t nserial,
+    float z, float sfloor) {
     __shared__ uint32_t bstart[256];
     __shared__ uint32_t blo[256];
     __shared__ uint32_t nfull;
+    __shared__ uint32_t rows[kChainLds];  // block-end rows of the chain, a chunk at a time
+    __shared__ uint32_t cB, cblk, cstop, cleft;
     if (ctrl[0] != 0u) {
         if (fin && threadIdx.x == 0) fin[1] = 0u;  // (serial_states_kernel: nothing)
         return;
@@ -1528,25 +1538,93 @@ __global__ __launch_bounds__(256) void serial_walk_finish_kernel(
     for (uint32_t blk = threadIdx.x; blk < nb; blk += blockDim.x)
         blo[blk] = serial_lo(M, a, blk * R, K, depth, nserial);
     __syncthreads();
+    // The chain through the block ends, one dependent lookup per block: the
+    // workgroup stages the block-end rows in LDS a chunk of blocks at a time
+    // (independent, coalesced loads) and lane 0 follows the chain there, not
+    // through one L2 round trip per block (c_raytracer 960x540x16: 98 us per
+    // iteration for 256 blocks)
     if (threadIdx.x == 0) {
-        uint32_t B = 0, blk = 0;
-        for (; blk < nb; ++blk) {
-            const uint32_t l = blo[blk];
-            const uint32_t e = (B >= l && B - l < K) ? bend[(size_t)blk * K + (B - l)] : kWalkInvalid;
-            if (e == kWalkInvalid) break;
-            bstart[blk] = B;
-            if (fin) fin[4 + blk] = blk * K + (B - l);  // the block's path column
-            B = e;
+        cB = 0;
+        cblk = 0;
+        cstop = 0;
+        cleft = 0;
+    }
+    const bool staged = K <= kChainLds;  // (wider windows: straight from bend)
+    const uint32_t rpc = staged ? kChainLds / K : nb;  // blocks per chunk
+    for (uint32_t c0 = 0; c0 < nb; c0 += rpc) {
+        const uint32_t c1 = min(nb, c0 + rpc);
+        __syncthreads();
+        if (cstop) break;
+        // (16-B loads from the 16-B aligned word below the chunk, 12 in flight
+        // per thread: a 48 KB chunk in one round trip; bend has 4 words of
+        // padding, render.h serial_walk_block)
+        const uint32_t cn = staged ? (c1 - c0) * K : 0u;
+        const size_t base = (size_t)c0 * K;
+        const uint32_t o = (uint32_t)(base & 3u);
+        const uint4 *src = reinterpret_cast<const uint4 *>(bend + (base - o));
+        const uint32_t nv = (cn + o + 3u) / 4u;
+        for (uint32_t v0 = 0; v0 < nv; v0 += 12u * blockDim.x) {
+            uint4 x[12];
+#pragma unroll
+            for (uint32_t q = 0; q < 12; ++q) {
+                const uint32_t v = v0 + q * blockDim.x + threadIdx.x;
+                x[q] = v < nv ? src[v] : make_uint4(0u, 0u, 0u, 0u);
+            }
+#pragma unroll
+            for (uint32_t q = 0; q < 12; ++q) {
+                const uint32_t v = v0 + q * blockDim.x + threadIdx.x;
+                const uint32_t w[4] = {x[q].x, x[q].y, x[q].z, x[q].w};
+#pragma unroll
+                for (uint32_t e = 0; e < 4; ++e) {
+                    const uint32_t i = 4u * v + e;  // word of the aligned run
+                    if (v < nv && i >= o && i - o < cn) rows[i - o] = w[e];
+                }
+            }
         }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            uint32_t B = cB, blk = c0;
+            for (; blk < c1; ++blk) {
+                const uint32_t l = blo[blk];
+                const uint32_t e = !(B >= l && B - l < K) ? kWalkInvalid
+                                   : staged          ? rows[(blk - c0) * K + (B - l)]
+                                                     : bend[(size_t)blk * K + (B - l)];
+                if (e & kWalkLeft) {
+                    cleft = e == kWalkInvalid ? 0u : e & ~kWalkLeft;  // samples resolved in blk
+                    break;
+                }
+                bstart[blk] = B;
+                if (fin) fin[4 + blk] = blk * K + (B - l);  // the block's path column
+                B = e;
+            }
+            cB = B;
+            cblk = blk;
+            cstop = blk < c1 ? 1u : 0u;
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t B = cB, blk = cblk;
         nfull = blk;
+        uint32_t done = min(blk * R, n);
         if (fin) {
+            if (blk < nb && cleft > 0u) {
+                // the path leaves a window inside this block, after cleft
+                // samples whose states the block walk's path holds, as it
+                // holds the start offset of the sample that left
+                const uint32_t col = blk * K + (B - blo[blk]);
+                fin[4 + blk] = col;
+                B = path[(size_t)cleft * nb * K + col];
+                done = blk * R + cleft;
+            }
             fin[0] = a;
             fin[1] = blk;
             fin[2] = nb * K;
-            fin[3] = n;  // (the last block may be short)
+            fin[3] = done;  // the states to gather: samples [0, done) of the iteration
         }
-        uint32_t done = min(blk * R, n);
-        if (blk < nb) {
+        if (blk < nb && fin) {
+            ctrl[6] += 1u;
+        } else if (blk < nb) {
             // the path leaves a window inside this block: resolve it lane-serially
             // up to that sample (the window of the block's first sample holds B:
             // it was the previous block's valid end, or 0)
@@ -1604,8 +1682,7 @@ __global__ __launch_bounds__(256) void serial_states_kernel(const uint32_t *__re
                                                             const uint32_t *__restrict__ win,
                                                             uint32_t *__restrict__ states, uint32_t R) {
     const uint32_t jl = blockIdx.x * blockDim.x + threadIdx.x;
-    const uint32_t nfull = fin[1];
-    if (jl >= nfull * R || jl >= fin[3]) return;
+    if (jl >= fin[3]) return;
     const uint32_t blk = jl / R;
     const uint32_t B = path[(size_t)(jl - blk * R) * fin[2] + fin[4 + blk]];
     states[fin[0] + jl] = win[2u * jl + 3u * B];
@@ -1839,8 +1916,8 @@ hipError_t launch_serial_walk(uint32_t *ctrl, const float *table, SerialPred M, 
     hipLaunchKernelGGL(serial_walk_blocks_kernel, dim3((uint32_t)((nt + 255) / 256)), dim3(256), 0, stream,
                        ctrl, table, M, bend, path, L, K, R, depth, nserial);
     hipLaunchKernelGGL(serial_walk_finish_kernel, dim3(1), dim3(256), 0, stream, ctrl, table, M, V, npix,
-                       spp ? spp : 1u, win, bend, states, path ? fin : nullptr, L, K, R, depth, nserial, z,
-                       sfloor);
+                       spp ? spp : 1u, win, bend, path, states, path ? fin : nullptr, L, K, R, depth, nserial,
+                       z, sfloor);
     if (path)
         hipLaunchKernelGGL(serial_states_kernel, dim3((L + 255) / 256), dim3(256), 0, stream, fin, path, win,
                            states, R);

@@ -898,7 +898,7 @@ static int serial_find_states(WorldState &w, const CameraModel &cam, size_t widt
             K0 = (uint32_t)std::min<double>((double)K, std::ceil(w0) + 2.0 * depth + 2.0);
         }
         HIP_TRY(grow(d->swin, d->swin_cap, wlen));
-        HIP_TRY(grow(d->sbend, d->sbend_cap, (L + R_walk - 1) / R_walk * K));
+        HIP_TRY(grow(d->sbend, d->sbend_cap, (L + R_walk - 1) / R_walk * K + 4));  // (+4: the chain's 16-B loads)
         // recorded block paths: the states of resolved samples become a gather
         const bool gather = env_u64("RT_AMD_SERIAL_GATHER", 1) != 0;
         if (gather) {
