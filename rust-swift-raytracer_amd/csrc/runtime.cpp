@@ -818,8 +818,14 @@ static int serial_find_states(WorldState &w, const CameraModel &cam, size_t widt
         // 1. per-pixel mean scatter counts from R counter-seeded traces per
         // sample, reduced on the device (per-pixel moments, then prefix sums
         // over pixels): no per-sample table and no host pass over the samples
+        // (RT_AMD_SERIAL_EST traces per pixel: the means' error adds to every
+        // window's deviation, sweep on the 960x540x16 frames at z 1.5:
+        // c_raytracer / RTOW / world.txt 32 -> 457 / 315 / - ms, 128 -> 418 /
+        // 281 / 364, 256 -> 416 / 285 / 360, 512 -> 427 / 281 / -; z 1.2 and
+        // 1.0 cost more at every EST, 1.8 and 2.1 as much or more)
+        const uint64_t est = std::max<uint64_t>(1, env_u64("RT_AMD_SERIAL_EST", 128));
         const uint64_t R = std::max<uint64_t>(
-            1, std::min<uint64_t>({(32 + spp - 1) / spp, 16, 0x7FFFFFFFull / N}));
+            1, std::min<uint64_t>({(est + spp - 1) / spp, 64, 0x7FFFFFFFull / N}));
         const uint64_t npix = (uint64_t)width * height;
         const double per = (double)(spp * R);
         const uint64_t L = std::max<uint64_t>(1, std::min<uint64_t>(env_u64("RT_AMD_SERIAL_CHUNK", 16384), N));
