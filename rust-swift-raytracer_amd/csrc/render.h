@@ -222,10 +222,13 @@ hipError_t launch_assemble(const uint32_t *gathered, uint32_t *out, uint32_t wid
                            uint32_t row_block, uint32_t nranks, uint32_t max_rows,
                            hipStream_t stream);
 // variant: 0 brute force, 1 BVH from global memory, 2 BVH staged in LDS;
-// step: the sliced-walk kernel (TraceParams::step); tri: the scene has triangles
+// step: the sliced-walk kernel (TraceParams::step); mesh: trace_mesh_kind
 // workgroups per CU of one trace_kernel instance (count: the counting variant)
-hipError_t trace_occupancy(int *blocks_per_cu, int variant, size_t lds_bytes, bool step, bool tri,
+hipError_t trace_occupancy(int *blocks_per_cu, int variant, size_t lds_bytes, bool step, int mesh,
                            bool count);
+// The kernel family of a scene: 0 no triangles, 1 triangles searched by brute
+// force (no triangle tree), 2 triangle trees (TraceParams::tnodes != 0)
+inline int trace_mesh_kind(bool triangles, bool tree) { return !triangles ? 0 : tree ? 2 : 1; }
 size_t trace_lds_bytes(const TraceParams &p);
 // threads per trace workgroup: LDS-tree kernels (sphere-only scenes or not) vs global
 uint32_t trace_block_threads(bool lds, bool mesh);

@@ -695,9 +695,9 @@ __device__ __forceinline__ void resolve_chunk(const TraceParams &p, const float 
 // kSerial: the SERIAL-mode passes (render.h kRngSerial*): jobs are (sample,
 // variant) pairs and store scatter counts -- a separate instance, so the frame
 // kernels carry none of its registers.
-template <bool kBvh, bool kLds, bool kStep, bool kMesh, bool kCount, bool kSerial = false>
-__global__ __launch_bounds__(kLds ? (kMesh ? RT_LDS_BLOCK_MESH : RT_LDS_BLOCK_SPHERES) : 256)
-__attribute__((amdgpu_waves_per_eu((kMesh && !kCount) ? RT_WAVES_PER_EU_MESH : RT_WAVES_PER_EU, 8)))
+template <bool kBvh, bool kLds, bool kStep, int kMesh, bool kCount, bool kSerial = false>
+__global__ __launch_bounds__(kLds ? (kMesh != 0 ? RT_LDS_BLOCK_MESH : RT_LDS_BLOCK_SPHERES) : 256)
+__attribute__((amdgpu_waves_per_eu((kMesh != 0 && !kCount) ? RT_WAVES_PER_EU_MESH : RT_WAVES_PER_EU, 8)))
 void trace_kernel(TraceParams p) {
     // SERIAL count passes: the walk of the previous pass set the first sample
     // and this iteration's candidates per sample (ctrl[5], <= the launch's K)
@@ -939,9 +939,9 @@ void trace_kernel(TraceParams p) {
                 tri_t = __builtin_inff();
                 tri_i = -1;
                 phase = kShade;
-                if (!kMesh) {
+                if (kMesh == 0) {
                     // no triangles: Mesh::hit finds nothing
-                } else if (p.tnodes != 0) {
+                } else if (kMesh == 2) {  // (p.tnodes != 0)
                     const bool cam = bounce == 0 && p.cam_nnodes != 0;
                     if (tri_begin(p, org, dir, best_t, cam, e, tri_t, tri_i, tri_in, tri_done)) {
                         // (the lists index the camera-origin records, which exist
@@ -959,12 +959,12 @@ void trace_kernel(TraceParams p) {
                 }
             }
             bool tri_now = true;
-            if (kMesh && p.tri_walk_min != 0) {
+            if (kMesh == 2 && p.tri_walk_min != 0) {
                 const uint32_t nwalk = (uint32_t)__popcll(__ballot(phase == kTri));
                 const uint32_t nother = (uint32_t)__popcll(__ballot(phase != kTri && !done));
                 tri_now = nwalk >= p.tri_walk_min || nother == 0;
             }
-            if (kMesh && phase == kTri && tri_now) {
+            if (kMesh == 2 && phase == kTri && tri_now) {
                 if (kStep) budget = max(budget, p.steps / 2u);  // a lane that just left the sphere walk
                 const bool cam = bounce == 0 && p.cam_nnodes != 0;
                 const F3 dlt2 = f3(2.0f * (org.x - p.tbvh_oc[0]), 2.0f * (org.y - p.tbvh_oc[1]),
@@ -1120,7 +1120,7 @@ void trace_kernel(TraceParams p) {
                     rleft[k] -= n;
                     if (n != 0 && rleft[k] == 0) {
                         if (!(p.ablate & 2u))
-                            resolve_chunk<!kMesh>(p, sbase, pstride, k << p.ring_shift, rbase[k],
+                            resolve_chunk<kMesh != 2>(p, sbase, pstride, k << p.ring_shift, rbase[k],
                                                   rlen[k], lane);
                         rfree |= 1u << k;
                     }
@@ -1346,11 +1346,11 @@ size_t trace_lds_bytes(const TraceParams &p) {
     return (size_t)p.nnodes * 48 + (size_t)p.nprims * 20 + (size_t)p.nsph_padded * 36;
 }
 
-template <bool kStep, bool kMesh, bool kCount, bool kSerial>
+template <bool kStep, int kMesh, bool kCount, bool kSerial>
 static void launch_trace_t(const TraceParams &p, uint32_t blocks, hipStream_t stream) {
     if (p.nnodes && p.use_lds)
         hipLaunchKernelGGL((trace_kernel<true, true, kStep, kMesh, kCount, kSerial>), dim3(blocks),
-                           dim3(trace_block_threads(true, kMesh)),
+                           dim3(trace_block_threads(true, kMesh != 0)),
                            trace_lds_bytes(p), stream, p);
     else if (p.nnodes)
         hipLaunchKernelGGL((trace_kernel<true, false, kStep, kMesh, kCount, kSerial>), dim3(blocks),
@@ -1360,15 +1360,19 @@ static void launch_trace_t(const TraceParams &p, uint32_t blocks, hipStream_t st
                            dim3(256), 0, stream, p);
 }
 
+// kMesh: 0 no triangles, 1 brute-force triangles (no triangle tree: small
+// meshes), 2 triangle trees -- the tree walk's registers only where it runs
 template <bool kCount, bool kSerial>
 static void launch_trace_c(const TraceParams &p, uint32_t blocks, hipStream_t stream) {
-    const bool tri = p.ntri != 0;
+    const int mesh = trace_mesh_kind(p.ntri != 0, p.tnodes != 0);
     if (p.step) {
-        if (tri) launch_trace_t<true, true, kCount, kSerial>(p, blocks, stream);
-        else launch_trace_t<true, false, kCount, kSerial>(p, blocks, stream);
+        if (mesh == 2) launch_trace_t<true, 2, kCount, kSerial>(p, blocks, stream);
+        else if (mesh == 1) launch_trace_t<true, 1, kCount, kSerial>(p, blocks, stream);
+        else launch_trace_t<true, 0, kCount, kSerial>(p, blocks, stream);
     } else {
-        if (tri) launch_trace_t<false, true, kCount, kSerial>(p, blocks, stream);
-        else launch_trace_t<false, false, kCount, kSerial>(p, blocks, stream);
+        if (mesh == 2) launch_trace_t<false, 2, kCount, kSerial>(p, blocks, stream);
+        else if (mesh == 1) launch_trace_t<false, 1, kCount, kSerial>(p, blocks, stream);
+        else launch_trace_t<false, 0, kCount, kSerial>(p, blocks, stream);
     }
 }
 
@@ -1391,12 +1395,12 @@ hipError_t launch_resolve_ex(const float *samples, uint32_t *out, uint32_t npix,
     return hipGetLastError();
 }
 
-template <bool kStep, bool kMesh, bool kCount>
+template <bool kStep, int kMesh, bool kCount>
 static hipError_t trace_occupancy_t(int *blocks_per_cu, int variant, size_t lds_bytes) {
     if (variant == 2)
         return hipOccupancyMaxActiveBlocksPerMultiprocessor(
             blocks_per_cu, trace_kernel<true, true, kStep, kMesh, kCount>,
-            trace_block_threads(true, kMesh), lds_bytes);
+            trace_block_threads(true, kMesh != 0), lds_bytes);
     if (variant == 1)
         return hipOccupancyMaxActiveBlocksPerMultiprocessor(
             blocks_per_cu, trace_kernel<true, false, kStep, kMesh, kCount>, 256, 0);
@@ -1406,18 +1410,20 @@ static hipError_t trace_occupancy_t(int *blocks_per_cu, int variant, size_t lds_
 
 template <bool kCount>
 static hipError_t trace_occupancy_c(int *blocks_per_cu, int variant, size_t lds_bytes, bool step,
-                                    bool tri) {
+                                    int mesh) {
     if (step)
-        return tri ? trace_occupancy_t<true, true, kCount>(blocks_per_cu, variant, lds_bytes)
-                   : trace_occupancy_t<true, false, kCount>(blocks_per_cu, variant, lds_bytes);
-    return tri ? trace_occupancy_t<false, true, kCount>(blocks_per_cu, variant, lds_bytes)
-               : trace_occupancy_t<false, false, kCount>(blocks_per_cu, variant, lds_bytes);
+        return mesh == 2   ? trace_occupancy_t<true, 2, kCount>(blocks_per_cu, variant, lds_bytes)
+               : mesh == 1 ? trace_occupancy_t<true, 1, kCount>(blocks_per_cu, variant, lds_bytes)
+                           : trace_occupancy_t<true, 0, kCount>(blocks_per_cu, variant, lds_bytes);
+    return mesh == 2   ? trace_occupancy_t<false, 2, kCount>(blocks_per_cu, variant, lds_bytes)
+           : mesh == 1 ? trace_occupancy_t<false, 1, kCount>(blocks_per_cu, variant, lds_bytes)
+                       : trace_occupancy_t<false, 0, kCount>(blocks_per_cu, variant, lds_bytes);
 }
 
-hipError_t trace_occupancy(int *blocks_per_cu, int variant, size_t lds_bytes, bool step, bool tri,
+hipError_t trace_occupancy(int *blocks_per_cu, int variant, size_t lds_bytes, bool step, int mesh,
                            bool count) {
-    return count ? trace_occupancy_c<true>(blocks_per_cu, variant, lds_bytes, step, tri)
-                 : trace_occupancy_c<false>(blocks_per_cu, variant, lds_bytes, step, tri);
+    return count ? trace_occupancy_c<true>(blocks_per_cu, variant, lds_bytes, step, mesh)
+                 : trace_occupancy_c<false>(blocks_per_cu, variant, lds_bytes, step, mesh);
 }
 
 // ------------------------------------------------------------ SERIAL mode

@@ -107,7 +107,9 @@ static int device_for(WorldState &w, int want, DeviceState *&out) {
         hipDeviceProp_t prop;
         HIP_TRY(hipGetDeviceProperties(&prop, dev));
         d->num_cus = prop.multiProcessorCount;
-        const bool tri = w.packed.ntri > 0;  // the kTri kernels (render.hip)
+        // the scene's kernel family (render.h trace_mesh_kind; frames rendered with
+        // RT_ACCEL_BRUTE run the brute-force triangle kernels on these figures)
+        const int tri = trace_mesh_kind(w.packed.ntri > 0, !w.tbvh.nodes.empty());
         for (int c = 0; c < 2; ++c)
             for (int st = 0; st < 2; ++st) {
                 HIP_TRY(trace_occupancy(&d->blocks_per_cu[c][st], 0, 0, st, tri, c));
