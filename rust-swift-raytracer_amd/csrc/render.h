@@ -130,6 +130,8 @@ struct TraceParams {
     // clamped to nserial - 1
     const uint32_t *win;      // kRngSerialCount: stream states from sample cbase's start on
     SerialPred sM;            // kRngSerialCount: the predicted scatter counts (per pixel)
+    const uint32_t *slo;      // kRngSerialCount (optional): serial_lo of each launch sample,
+                              // tabulated by serial_window_kernel
     const uint32_t *ctrl;     // serial control block (kRngSerialCount: cbase = ctrl[4];
                               // ctrl[0] != 0, the frame is resolved: exit at once)
     uint32_t cbase;           // first frame sample of the launch
@@ -189,8 +191,12 @@ size_t serial_scan_scratch(uint32_t npix);
 // bits), iterations, a = first unresolved sample, candidates per sample of the
 // next iteration (0: the launch's K), iterations that stopped short, 0}.
 // jump: 64 x 32 u32, column c of M^(2^i) (xorshift32 is linear over GF(2)).  Window: win[i] = xorshift32^i(ctrl[1]) for i < n.
+// lo (optional): L u32, the iteration's window bases serial_lo(a, jl) with the
+// iteration's K (ctrl[5] when set, else K), for the count pass
+// (TraceParams::slo) and the walks.
 hipError_t launch_serial_window(const uint32_t *ctrl, const uint32_t *jump, uint32_t *win, uint32_t n,
-                                hipStream_t stream);
+                                SerialPred M, uint32_t *lo, uint32_t L, uint32_t K, uint32_t depth,
+                                uint32_t nserial, hipStream_t stream);
 // Walk: from sample a = ctrl[4], follows the true path through the candidate
 // table (b of chunk sample jl at candidate k = table[jl * K + k], plane 0 of
 // the slab) as far as it stays inside the candidate windows (at least one
@@ -209,8 +215,9 @@ uint32_t serial_walk_block(uint32_t L);
 // pass and the walks use ctrl[5] when it is set.
 hipError_t launch_serial_walk(uint32_t *ctrl, const float *table, SerialPred M, const double *V,
                               uint32_t npix, uint32_t spp, float z, float sfloor, const uint32_t *win,
-                              uint32_t *states, uint32_t *bend, uint32_t *path, uint32_t *fin, uint32_t L,
-                              uint32_t K, uint32_t depth, uint32_t nserial, hipStream_t stream);
+                              uint32_t *states, uint32_t *bend, uint32_t *path, uint32_t *fin,
+                              const uint32_t *lo, uint32_t L, uint32_t K, uint32_t depth, uint32_t nserial,
+                              hipStream_t stream);
 // inv_spp = 1.0 / (spp as f32) computed from the signed spp (common.rs:345).
 hipError_t launch_resolve_ex(const float *samples, uint32_t *out, uint32_t npix, uint32_t spp,
                              float inv_spp, uint32_t width, uint32_t slab_row0,

@@ -557,8 +557,9 @@ __device__ __forceinline__ uint32_t serial_start(const TraceParams &p, uint32_t 
     const uint32_t jl = fdiv(job, p.div_spp);
     const uint32_t k = job - jl * p.spp;
     if (p.mode == kRngSerialCount)
-        return p.win[2u * jl + 3u * (serial_lo(p.sM, p.cbase, jl, p.spp, (p.max_draws - 2u) / 3u,
-                                               p.nserial) + k)];
+        return p.win[2u * jl + 3u * ((p.slo ? p.slo[jl]
+                                            : serial_lo(p.sM, p.cbase, jl, p.spp, (p.max_draws - 2u) / 3u,
+                                                        p.nserial)) + k)];
     if (p.mode == kRngSerialCheck) return p.win[p.cbase + jl];
     return counter_seed(p.seed, (uint64_t)(p.cbase + jl) * p.spp + k);
 }
@@ -1446,11 +1447,25 @@ __device__ __forceinline__ uint32_t gf2_apply(const uint32_t *cols, uint32_t x) 
 // Window: thread t writes win[16t, 16t + 16): one jump to 16t (matrices of the
 // set bits), then plain xorshift steps.
 constexpr uint32_t kWinPerThread = 16;
+// It also tabulates the iteration's window bases lo[jl] = serial_lo(a, jl) for
+// jl < L (a = ctrl[4], K = the iteration's candidates), which the count pass
+// and the walks then load instead of evaluating M twice per step.
 __global__ __launch_bounds__(256) void serial_window_kernel(const uint32_t *__restrict__ ctrl,
                                                             const uint32_t *__restrict__ jump,
-                                                            uint32_t *__restrict__ win, uint32_t n) {
+                                                            uint32_t *__restrict__ win, uint32_t n,
+                                                            SerialPred M, uint32_t *__restrict__ lo,
+                                                            uint32_t L, uint32_t Kmax, uint32_t depth,
+                                                            uint32_t nserial) {
+    if (ctrl[0] != 0u) return;
+    if (lo != nullptr) {
+        const uint32_t k = ctrl[5];
+        const uint32_t K = k != 0u && k < Kmax ? k : Kmax;  // (serial_k)
+        const uint32_t a = ctrl[4];
+        for (uint32_t jl = blockIdx.x * blockDim.x + threadIdx.x; jl < L; jl += gridDim.x * blockDim.x)
+            lo[jl] = serial_lo(M, a, jl, K, depth, nserial);
+    }
     const uint32_t i0 = (blockIdx.x * blockDim.x + threadIdx.x) * kWinPerThread;
-    if (ctrl[0] != 0u || i0 >= n) return;
+    if (i0 >= n) return;
     uint32_t x = ctrl[1];
     for (uint32_t b = 0; (i0 >> b) != 0u; ++b)
         if ((i0 >> b) & 1u) x = gf2_apply(jump + 32u * b, x);
@@ -1478,8 +1493,8 @@ constexpr uint32_t kWalkLeft = 0x80000000u;  // bend: the walk left a window (of
 constexpr uint32_t kChainLds = 12288;  // u32 of block-end rows staged per chunk (48 KB)
 __device__ __forceinline__ uint32_t walk_step(const float *table, const SerialPred &M, uint32_t a,
                                               uint32_t K, uint32_t depth, uint32_t nserial, uint32_t jl,
-                                              uint32_t B) {
-    const uint32_t l = serial_lo(M, a, jl, K, depth, nserial);
+                                              uint32_t B, const uint32_t *lo = nullptr) {
+    const uint32_t l = lo ? lo[jl] : serial_lo(M, a, jl, K, depth, nserial);
     const float b = (B >= l && B - l < K) ? table[(size_t)jl * K + (B - l)] : -1.0f;
     return b >= 0.0f ? B + (uint32_t)b : kWalkInvalid;
 }
@@ -1495,8 +1510,8 @@ __device__ __forceinline__ uint32_t serial_k(const uint32_t *ctrl, uint32_t K) {
 // of the true path are a gather (serial_states_kernel), not a re-walk
 __global__ __launch_bounds__(256) void serial_walk_blocks_kernel(
     const uint32_t *__restrict__ ctrl, const float *__restrict__ table, SerialPred M,
-    uint32_t *__restrict__ bend, uint32_t *__restrict__ path, uint32_t L, uint32_t K, uint32_t R,
-    uint32_t depth, uint32_t nserial) {
+    uint32_t *__restrict__ bend, uint32_t *__restrict__ path, const uint32_t *__restrict__ lo, uint32_t L,
+    uint32_t K, uint32_t R, uint32_t depth, uint32_t nserial) {
     if (ctrl[0] != 0u) return;
     K = serial_k(ctrl, K);
     const uint32_t a = ctrl[4];
@@ -1507,11 +1522,12 @@ __global__ __launch_bounds__(256) void serial_walk_blocks_kernel(
     const uint32_t blk = t / K, k0 = t - blk * K;
     const uint32_t j0 = blk * R, j1 = min(j0 + R, n);
     const size_t stride = (size_t)nb * K;
-    uint32_t B = serial_lo(M, a, j0, K, depth, nserial) + k0;
+    uint32_t B = (lo ? lo[j0] : serial_lo(M, a, j0, K, depth, nserial)) + k0;
     uint32_t jl = j0;
+#pragma unroll 4
     for (; jl < j1; ++jl) {
         if (path) path[(size_t)(jl - j0) * stride + t] = B;
-        const uint32_t nB = walk_step(table, M, a, K, depth, nserial, jl, B);
+        const uint32_t nB = walk_step(table, M, a, K, depth, nserial, jl, B, lo);
         if (nB == kWalkInvalid) break;
         B = nB;
     }
@@ -1524,8 +1540,8 @@ __global__ __launch_bounds__(256) void serial_walk_finish_kernel(
     uint32_t *__restrict__ ctrl, const float *__restrict__ table, SerialPred M,
     const double *__restrict__ V, uint32_t npix, uint32_t spp, const uint32_t *__restrict__ win,
     const uint32_t *__restrict__ bend, const uint32_t *__restrict__ path, uint32_t *__restrict__ states,
-    uint32_t *__restrict__ fin, uint32_t L, uint32_t Kmax, uint32_t R, uint32_t depth, uint32_t nserial,
-    float z, float sfloor) {
+    uint32_t *__restrict__ fin, const uint32_t *__restrict__ lo, uint32_t L, uint32_t Kmax, uint32_t R,
+    uint32_t depth, uint32_t nserial, float z, float sfloor) {
     __shared__ uint32_t bstart[256];
     __shared__ uint32_t blo[256];
     __shared__ uint32_t nfull;
@@ -1542,7 +1558,7 @@ __global__ __launch_bounds__(256) void serial_walk_finish_kernel(
     // every block's window base at once (they do not depend on the path), so
     // the chain below is one dependent load per block
     for (uint32_t blk = threadIdx.x; blk < nb; blk += blockDim.x)
-        blo[blk] = serial_lo(M, a, blk * R, K, depth, nserial);
+        blo[blk] = lo ? lo[blk * R] : serial_lo(M, a, blk * R, K, depth, nserial);
     __syncthreads();
     // The chain through the block ends, one dependent lookup per block: the
     // workgroup stages the block-end rows in LDS a chunk of blocks at a time
@@ -1636,7 +1652,7 @@ __global__ __launch_bounds__(256) void serial_walk_finish_kernel(
             // it was the previous block's valid end, or 0)
             const uint32_t j1 = min(blk * R + R, n);
             for (uint32_t jl = blk * R; jl < j1; ++jl) {
-                const uint32_t nB = walk_step(table, M, a, K, depth, nserial, jl, B);
+                const uint32_t nB = walk_step(table, M, a, K, depth, nserial, jl, B, lo);
                 if (nB == kWalkInvalid) break;
                 states[a + jl] = win[2u * jl + 3u * B];
                 B = nB;
@@ -1674,7 +1690,7 @@ __global__ __launch_bounds__(256) void serial_walk_finish_kernel(
         const uint32_t j1 = min(blk * R + R, n);
         for (uint32_t jl = blk * R; jl < j1; ++jl) {
             states[a + jl] = win[2u * jl + 3u * B];
-            B = walk_step(table, M, a, K, depth, nserial, jl, B);
+            B = walk_step(table, M, a, K, depth, nserial, jl, B, lo);
         }
     }
 }
@@ -1898,11 +1914,12 @@ hipError_t launch_serial_tables(double *tab, double *scratch, uint32_t npix, uin
 }
 
 hipError_t launch_serial_window(const uint32_t *ctrl, const uint32_t *jump, uint32_t *win, uint32_t n,
-                                hipStream_t stream) {
+                                SerialPred M, uint32_t *lo, uint32_t L, uint32_t K, uint32_t depth,
+                                uint32_t nserial, hipStream_t stream) {
     if (!n) return hipSuccess;
-    const uint32_t threads = (n + kWinPerThread - 1) / kWinPerThread;
+    const uint32_t threads = std::max((n + kWinPerThread - 1) / kWinPerThread, lo ? std::min(L, 1u << 16) : 0u);
     hipLaunchKernelGGL(serial_window_kernel, dim3((threads + 255) / 256), dim3(256), 0, stream, ctrl,
-                       jump, win, n);
+                       jump, win, n, M, lo, L, K, depth, nserial);
     return hipGetLastError();
 }
 
@@ -1913,17 +1930,18 @@ uint32_t serial_walk_block(uint32_t L) {
 
 hipError_t launch_serial_walk(uint32_t *ctrl, const float *table, SerialPred M, const double *V,
                               uint32_t npix, uint32_t spp, float z, float sfloor, const uint32_t *win,
-                              uint32_t *states, uint32_t *bend, uint32_t *path, uint32_t *fin, uint32_t L,
-                              uint32_t K, uint32_t depth, uint32_t nserial, hipStream_t stream) {
+                              uint32_t *states, uint32_t *bend, uint32_t *path, uint32_t *fin,
+                              const uint32_t *lo, uint32_t L, uint32_t K, uint32_t depth, uint32_t nserial,
+                              hipStream_t stream) {
     if (!L) return hipSuccess;
     const uint32_t R = serial_walk_block(L);
     const uint64_t nt = (uint64_t)((L + R - 1) / R) * K;
     if (!fin) path = nullptr;
     hipLaunchKernelGGL(serial_walk_blocks_kernel, dim3((uint32_t)((nt + 255) / 256)), dim3(256), 0, stream,
-                       ctrl, table, M, bend, path, L, K, R, depth, nserial);
+                       ctrl, table, M, bend, path, lo, L, K, R, depth, nserial);
     hipLaunchKernelGGL(serial_walk_finish_kernel, dim3(1), dim3(256), 0, stream, ctrl, table, M, V, npix,
-                       spp ? spp : 1u, win, bend, path, states, path ? fin : nullptr, L, K, R, depth, nserial,
-                       z, sfloor);
+                       spp ? spp : 1u, win, bend, path, states, path ? fin : nullptr, lo, L, K, R, depth,
+                       nserial, z, sfloor);
     if (path)
         hipLaunchKernelGGL(serial_states_kernel, dim3((L + 255) / 256), dim3(256), 0, stream, fin, path, win,
                            states, R);

@@ -54,7 +54,7 @@ DeviceState::~DeviceState() {
                     sph_shade, sph_kind, tbvh_nodes, tbvh_tris, tbvh_loose,
                     cam_nodes, cam_tris, ptl_off, ptl_items, spl, tile, gath,
                     sstates, stab, sscan, swin, sjump, sctrl, sbend, spath, sfin,
-                    gspl, gspl_rects, gspl_flag, scheck};
+                    gspl, gspl_rects, gspl_flag, scheck, slo};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
     for (hipEvent_t e : ev)
@@ -593,6 +593,7 @@ int render_frame(WorldState &w, const CameraModel &cam, size_t width, size_t hei
         p.nserial = (uint32_t)((uint64_t)width * height * spp);
         p.win = sp->win;
         p.sM = sp->M;
+        p.slo = sp->lo;
         p.ctrl = sp->ctrl;
         p.max_draws = 2u + 3u * (uint32_t)std::max(o.max_ray_bounces, 0);
         p.njobs = (uint32_t)njobs;
@@ -908,6 +909,7 @@ static int serial_find_states(WorldState &w, const CameraModel &cam, size_t widt
             K0 = (uint32_t)std::min<double>((double)K, std::ceil(w0) + 2.0 * depth + 2.0);
         }
         HIP_TRY(grow(d->swin, d->swin_cap, wlen));
+        HIP_TRY(grow(d->slo, d->slo_cap, L));
         HIP_TRY(grow(d->sbend, d->sbend_cap, (L + R_walk - 1) / R_walk * K + 4));  // (+4: the chain's 16-B loads)
         // recorded block paths: the states of resolved samples become a gather
         const bool gather = env_u64("RT_AMD_SERIAL_GATHER", 1) != 0;
@@ -943,15 +945,16 @@ static int serial_find_states(WorldState &w, const CameraModel &cam, size_t widt
             }
             const auto t0 = std::chrono::steady_clock::now();
             for (uint64_t q = 0; q < it; ++q) {
-                HIP_TRY(launch_serial_window(d->sctrl, d->sjump, d->swin, (uint32_t)wlen, s));
+                HIP_TRY(launch_serial_window(d->sctrl, d->sjump, d->swin, (uint32_t)wlen, pred, d->slo,
+                                             (uint32_t)L, (uint32_t)K, depth, (uint32_t)N, s));
                 const SerialPass sp{kRngSerialCount, 0u, (uint32_t)L, (uint32_t)K, d->swin, pred,
-                                    d->sctrl};
+                                    d->sctrl, d->slo};
                 rc = render_frame(w, cam, width, height, ob, nullptr, s, nullptr, &sp);
                 if (rc) return rc;
                 HIP_TRY(launch_serial_walk(d->sctrl, d->samples, pred, adapt ? Vdev : nullptr,
                                            (uint32_t)npix, (uint32_t)spp, (float)z, (float)serial_floor(spp * R),
                                            d->swin, d->sstates, d->sbend, gather ? d->spath : nullptr,
-                                           gather ? d->sfin : nullptr, (uint32_t)L, (uint32_t)K, depth,
+                                           gather ? d->sfin : nullptr, d->slo, (uint32_t)L, (uint32_t)K, depth,
                                            (uint32_t)N, s));
             }
             const auto t1 = std::chrono::steady_clock::now();

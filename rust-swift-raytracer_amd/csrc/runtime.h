@@ -72,6 +72,7 @@ struct DeviceState {
     uint32_t *sstates = nullptr;     size_t sstates_cap = 0;
     double *stab = nullptr;          size_t stab_cap = 0;   // prediction tables (render.h serial_tab_doubles)
     double *sscan = nullptr;         size_t sscan_cap = 0;  // their scan's scratch
+    uint32_t *slo = nullptr;         size_t slo_cap = 0;    // an iteration's window bases (launch_serial_window)
     uint32_t *swin = nullptr;        size_t swin_cap = 0;
     uint32_t *sbend = nullptr;       size_t sbend_cap = 0;
     uint32_t *spath = nullptr;       size_t spath_cap = 0;  // block walks' paths (L x K)
@@ -129,6 +130,7 @@ struct SerialPass {
     const uint32_t *win;
     SerialPred M;
     const uint32_t *ctrl;
+    const uint32_t *lo;       // kRngSerialCount (optional): tabulated window bases
 };
 
 // Renders rank's tile of a width x height frame into device memory d_out
