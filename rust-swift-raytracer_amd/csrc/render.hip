@@ -1464,11 +1464,16 @@ __global__ __launch_bounds__(256) void serial_window_kernel(const uint32_t *__re
         for (uint32_t jl = blockIdx.x * blockDim.x + threadIdx.x; jl < L; jl += gridDim.x * blockDim.x)
             lo[jl] = serial_lo(M, a, jl, K, depth, nserial);
     }
+    // the jump matrices this workgroup's threads need (bits of i0 below 32),
+    // staged in LDS: the jumps then read no global memory
+    __shared__ uint32_t jl_lds[32 * 32];
+    for (uint32_t i = threadIdx.x; i < 32u * 32u; i += blockDim.x) jl_lds[i] = jump[i];
+    __syncthreads();
     const uint32_t i0 = (blockIdx.x * blockDim.x + threadIdx.x) * kWinPerThread;
     if (i0 >= n) return;
     uint32_t x = ctrl[1];
     for (uint32_t b = 0; (i0 >> b) != 0u; ++b)
-        if ((i0 >> b) & 1u) x = gf2_apply(jump + 32u * b, x);
+        if ((i0 >> b) & 1u) x = gf2_apply(jl_lds + 32u * b, x);
     for (uint32_t q = 0; q < kWinPerThread && i0 + q < n; ++q) {
         win[i0 + q] = x;
         x ^= x << 13;
