@@ -202,8 +202,7 @@ hipError_t launch_serial_window(const uint32_t *ctrl, const uint32_t *jump, uint
 // the slab) as far as it stays inside the candidate windows (at least one
 // sample), writes those samples' start states to states[a + jl] and advances
 // ctrl (a, the state at a, resolved).  bend: scratch of
-// ceil(L / serial_walk_block(L)) * K + 4 u32 (the finish kernel's 16-B loads read up to
-// 3 words past the end).
+// ceil(L / serial_walk_block(L)) * K u32.
 uint32_t serial_walk_block(uint32_t L);
 // path, fin (optional, both or neither): scratch of ceil(L / R) R K u32 for the
 // block walks' recorded paths and 4 + 256 u32 for the chain's result; with
@@ -216,8 +215,11 @@ uint32_t serial_walk_block(uint32_t L);
 hipError_t launch_serial_walk(uint32_t *ctrl, const float *table, SerialPred M, const double *V,
                               uint32_t npix, uint32_t spp, float z, float sfloor, const uint32_t *win,
                               uint32_t *states, uint32_t *bend, uint32_t *path, uint32_t *fin,
-                              const uint32_t *lo, uint32_t L, uint32_t K, uint32_t depth, uint32_t nserial,
-                              hipStream_t stream);
+                              const uint32_t *lo, uint32_t *sbend, uint32_t *sB, uint32_t L, uint32_t K,
+                              uint32_t depth, uint32_t nserial, hipStream_t stream);
+// (lo: required; sbend, sB: scratch of serial_super_words(L, K) and ceil(L / R) K
+// u32 for the superblock chain)
+uint32_t serial_super_words(uint32_t L, uint32_t K);
 // inv_spp = 1.0 / (spp as f32) computed from the signed spp (common.rs:345).
 hipError_t launch_resolve_ex(const float *samples, uint32_t *out, uint32_t npix, uint32_t spp,
                              float inv_spp, uint32_t width, uint32_t slab_row0,

@@ -1483,19 +1483,23 @@ __global__ __launch_bounds__(256) void serial_window_kernel(const uint32_t *__re
 }
 
 // The walk through an iteration's candidate table (b of chunk sample jl at
-// candidate k = table[jl * K + k]; candidate k means B = serial_lo(jl) + k
-// scatters since sample a) in three dependent-load chains of ~32 steps
-// instead of one of L (a single-lane walk took ~0.7 ms per 2048 samples):
+// candidate k = table[jl * K + k]; candidate k means B = lo[jl] + k scatters
+// since sample a, lo = serial_lo tabulated by serial_window_kernel) in short
+// dependent-load chains instead of one of L:
 //   blocks: for every block of R samples and every candidate of its first
-//     sample, follow R samples: its end offset (or ~0 if it leaves a window);
-//   finish: one lane chains the block ends from B = 0 as far as they are
-//     valid (then lane by lane inside the block where the path left its
-//     window), then one lane per block re-walks its R samples from its known
-//     start, writing start states (win[2 jl + 3 B]); ctrl advances past the
-//     resolved samples (>= 1: sample a's own window always holds B = 0).
+//     sample, follow R samples: its end offset, or kWalkLeft | the samples
+//     walked before one left its window (the path of every walk recorded);
+//   super: for every group of kSuperBlocks blocks and every candidate of its
+//     first block, chain through the group's block ends (recording each
+//     block's start offset);
+//   finish: one lane chains the superblock ends from B = 0 as far as they
+//     are valid, the workgroup fills the full blocks' path columns from the
+//     recorded starts, and serial_states_kernel gathers the start states
+//     (win[2 jl + 3 B]) of every resolved sample from the recorded paths; ctrl
+//     advances past the resolved samples (>= 1: sample a's own window always
+//     holds B = 0).
 constexpr uint32_t kWalkInvalid = 0xFFFFFFFFu;
 constexpr uint32_t kWalkLeft = 0x80000000u;  // bend: the walk left a window (offsets stay below 2^31)
-constexpr uint32_t kChainLds = 12288;  // u32 of block-end rows staged per chunk (48 KB)
 __device__ __forceinline__ uint32_t walk_step(const float *table, const SerialPred &M, uint32_t a,
                                               uint32_t K, uint32_t depth, uint32_t nserial, uint32_t jl,
                                               uint32_t B, const uint32_t *lo = nullptr) {
@@ -1541,17 +1545,52 @@ __global__ __launch_bounds__(256) void serial_walk_blocks_kernel(
     bend[t] = jl == j1 ? B : kWalkLeft | (jl - j0);
 }
 
+// Superblocks of kSuperBlocks blocks: for every candidate start of a
+// superblock's first block, the chain through its blocks' ends (bend), so that
+// the finish kernel's chain is one dependent load per superblock.  sbend[sb *
+// K + k]: the superblock's end offset, or kWalkLeft | the block (within it)
+// where the chain stopped; sB[blk * K + k]: the offset at the start of its
+// block blk (nb * K u32, coalesced over k).
+constexpr uint32_t kSuperBlocks = 16;
+__global__ __launch_bounds__(256) void serial_walk_super_kernel(
+    const uint32_t *__restrict__ ctrl, const uint32_t *__restrict__ bend, const uint32_t *__restrict__ lo,
+    uint32_t *__restrict__ sbend, uint32_t *__restrict__ sB, uint32_t L, uint32_t Kmax, uint32_t R,
+    uint32_t nserial) {
+    if (ctrl[0] != 0u) return;
+    const uint32_t K = serial_k(ctrl, Kmax);
+    const uint32_t a = ctrl[4];
+    const uint32_t n = min(L, nserial - a);
+    const uint32_t nb = (n + R - 1) / R;
+    const uint32_t ns = (nb + kSuperBlocks - 1) / kSuperBlocks;
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= ns * K) return;
+    const uint32_t sb = t / K, k0 = t - sb * K;
+    const uint32_t b0 = sb * kSuperBlocks, b1 = min(nb, b0 + kSuperBlocks);
+    uint32_t B = lo[b0 * R] + k0;
+    uint32_t blk = b0;
+    for (; blk < b1; ++blk) {
+        sB[(size_t)blk * K + k0] = B;
+        const uint32_t l = lo[blk * R];
+        if (!(B >= l && B - l < K)) break;
+        const uint32_t e = bend[(size_t)blk * K + (B - l)];
+        if (e & kWalkLeft) break;
+        B = e;
+    }
+    sbend[t] = blk == b1 ? B : kWalkLeft | (blk - b0);
+}
+
 __global__ __launch_bounds__(256) void serial_walk_finish_kernel(
     uint32_t *__restrict__ ctrl, const float *__restrict__ table, SerialPred M,
     const double *__restrict__ V, uint32_t npix, uint32_t spp, const uint32_t *__restrict__ win,
     const uint32_t *__restrict__ bend, const uint32_t *__restrict__ path, uint32_t *__restrict__ states,
-    uint32_t *__restrict__ fin, const uint32_t *__restrict__ lo, uint32_t L, uint32_t Kmax, uint32_t R,
-    uint32_t depth, uint32_t nserial, float z, float sfloor) {
+    uint32_t *__restrict__ fin, const uint32_t *__restrict__ lo, const uint32_t *__restrict__ sbend,
+    const uint32_t *__restrict__ sB, uint32_t L, uint32_t Kmax, uint32_t R, uint32_t depth,
+    uint32_t nserial, float z, float sfloor) {
     __shared__ uint32_t bstart[256];
     __shared__ uint32_t blo[256];
     __shared__ uint32_t nfull;
-    __shared__ uint32_t rows[kChainLds];  // block-end rows of the chain, a chunk at a time
-    __shared__ uint32_t cB, cblk, cstop, cleft;
+    __shared__ uint32_t scol[256 / kSuperBlocks + 1];  // the chain's column in each superblock
+    __shared__ uint32_t cB, cblk, cleft;
     if (ctrl[0] != 0u) {
         if (fin && threadIdx.x == 0) fin[1] = 0u;  // (serial_states_kernel: nothing)
         return;
@@ -1560,74 +1599,48 @@ __global__ __launch_bounds__(256) void serial_walk_finish_kernel(
     const uint32_t a = ctrl[4];
     const uint32_t n = min(L, nserial - a);
     const uint32_t nb = (n + R - 1) / R;
-    // every block's window base at once (they do not depend on the path), so
-    // the chain below is one dependent load per block
+    const uint32_t ns = (nb + kSuperBlocks - 1) / kSuperBlocks;
     for (uint32_t blk = threadIdx.x; blk < nb; blk += blockDim.x)
         blo[blk] = lo ? lo[blk * R] : serial_lo(M, a, blk * R, K, depth, nserial);
     __syncthreads();
-    // The chain through the block ends, one dependent lookup per block: the
-    // workgroup stages the block-end rows in LDS a chunk of blocks at a time
-    // (independent, coalesced loads) and lane 0 follows the chain there, not
-    // through one L2 round trip per block (c_raytracer 960x540x16: 98 us per
-    // iteration for 256 blocks)
+    // The chain through the superblock ends: one dependent load per
+    // superblock (the block-by-block chain was 256 dependent L2 loads, 98 us
+    // per iteration on c_raytracer 960x540x16); where it stops, the block and
+    // its start offset come from the superblock's recorded block starts.
     if (threadIdx.x == 0) {
-        cB = 0;
-        cblk = 0;
-        cstop = 0;
-        cleft = 0;
+        uint32_t B = 0, sb = 0, blk = nb, left = 0;
+        for (; sb < ns; ++sb) {
+            const uint32_t b0 = sb * kSuperBlocks, l = blo[b0];
+            if (!(B >= l && B - l < K)) {  // outside the first block's window
+                blk = b0;
+                break;
+            }
+            const uint32_t col = sb * K + (B - l);
+            scol[sb] = col;
+            const uint32_t e = sbend[col];
+            if (e & kWalkLeft) {
+                blk = b0 + (e & ~kWalkLeft);
+                B = sB[(size_t)blk * K + (col - sb * K)];
+                const uint32_t lb = blo[blk];
+                if (B >= lb && B - lb < K) {
+                    const uint32_t eb = bend[(size_t)blk * K + (B - lb)];
+                    left = eb == kWalkInvalid ? 0u : eb & ~kWalkLeft;  // samples resolved in blk
+                }
+                break;
+            }
+            B = e;
+        }
+        cB = B;
+        cblk = blk;
+        cleft = left;
     }
-    const bool staged = K <= kChainLds;  // (wider windows: straight from bend)
-    const uint32_t rpc = staged ? kChainLds / K : nb;  // blocks per chunk
-    for (uint32_t c0 = 0; c0 < nb; c0 += rpc) {
-        const uint32_t c1 = min(nb, c0 + rpc);
-        __syncthreads();
-        if (cstop) break;
-        // (16-B loads from the 16-B aligned word below the chunk, 12 in flight
-        // per thread: a 48 KB chunk in one round trip; bend has 4 words of
-        // padding, render.h serial_walk_block)
-        const uint32_t cn = staged ? (c1 - c0) * K : 0u;
-        const size_t base = (size_t)c0 * K;
-        const uint32_t o = (uint32_t)(base & 3u);
-        const uint4 *src = reinterpret_cast<const uint4 *>(bend + (base - o));
-        const uint32_t nv = (cn + o + 3u) / 4u;
-        for (uint32_t v0 = 0; v0 < nv; v0 += 12u * blockDim.x) {
-            uint4 x[12];
-#pragma unroll
-            for (uint32_t q = 0; q < 12; ++q) {
-                const uint32_t v = v0 + q * blockDim.x + threadIdx.x;
-                x[q] = v < nv ? src[v] : make_uint4(0u, 0u, 0u, 0u);
-            }
-#pragma unroll
-            for (uint32_t q = 0; q < 12; ++q) {
-                const uint32_t v = v0 + q * blockDim.x + threadIdx.x;
-                const uint32_t w[4] = {x[q].x, x[q].y, x[q].z, x[q].w};
-#pragma unroll
-                for (uint32_t e = 0; e < 4; ++e) {
-                    const uint32_t i = 4u * v + e;  // word of the aligned run
-                    if (v < nv && i >= o && i - o < cn) rows[i - o] = w[e];
-                }
-            }
-        }
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            uint32_t B = cB, blk = c0;
-            for (; blk < c1; ++blk) {
-                const uint32_t l = blo[blk];
-                const uint32_t e = !(B >= l && B - l < K) ? kWalkInvalid
-                                   : staged          ? rows[(blk - c0) * K + (B - l)]
-                                                     : bend[(size_t)blk * K + (B - l)];
-                if (e & kWalkLeft) {
-                    cleft = e == kWalkInvalid ? 0u : e & ~kWalkLeft;  // samples resolved in blk
-                    break;
-                }
-                bstart[blk] = B;
-                if (fin) fin[4 + blk] = blk * K + (B - l);  // the block's path column
-                B = e;
-            }
-            cB = B;
-            cblk = blk;
-            cstop = blk < c1 ? 1u : 0u;
-        }
+    __syncthreads();
+    // the full blocks' start offsets and path columns, in parallel
+    for (uint32_t blk = threadIdx.x; blk < cblk; blk += blockDim.x) {
+        const uint32_t sb = blk / kSuperBlocks;
+        const uint32_t Bb = sB[(size_t)blk * K + (scol[sb] - sb * K)];
+        bstart[blk] = Bb;
+        if (fin) fin[4 + blk] = blk * K + (Bb - blo[blk]);  // the block's path column
     }
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -1928,6 +1941,11 @@ hipError_t launch_serial_window(const uint32_t *ctrl, const uint32_t *jump, uint
     return hipGetLastError();
 }
 
+uint32_t serial_super_words(uint32_t L, uint32_t K) {
+    const uint32_t nb = (L + serial_walk_block(L) - 1) / serial_walk_block(L);
+    return (nb + kSuperBlocks - 1) / kSuperBlocks * K;
+}
+
 uint32_t serial_walk_block(uint32_t L) {
     const uint32_t R = (L + 255) / 256;
     return R < 32u ? 32u : R;
@@ -1936,17 +1954,21 @@ uint32_t serial_walk_block(uint32_t L) {
 hipError_t launch_serial_walk(uint32_t *ctrl, const float *table, SerialPred M, const double *V,
                               uint32_t npix, uint32_t spp, float z, float sfloor, const uint32_t *win,
                               uint32_t *states, uint32_t *bend, uint32_t *path, uint32_t *fin,
-                              const uint32_t *lo, uint32_t L, uint32_t K, uint32_t depth, uint32_t nserial,
-                              hipStream_t stream) {
+                              const uint32_t *lo, uint32_t *sbend, uint32_t *sB, uint32_t L, uint32_t K,
+                              uint32_t depth, uint32_t nserial, hipStream_t stream) {
     if (!L) return hipSuccess;
     const uint32_t R = serial_walk_block(L);
-    const uint64_t nt = (uint64_t)((L + R - 1) / R) * K;
+    const uint32_t nb = (L + R - 1) / R;
+    const uint64_t nt = (uint64_t)nb * K;
+    const uint64_t nst = (uint64_t)((nb + kSuperBlocks - 1) / kSuperBlocks) * K;
     if (!fin) path = nullptr;
     hipLaunchKernelGGL(serial_walk_blocks_kernel, dim3((uint32_t)((nt + 255) / 256)), dim3(256), 0, stream,
                        ctrl, table, M, bend, path, lo, L, K, R, depth, nserial);
+    hipLaunchKernelGGL(serial_walk_super_kernel, dim3((uint32_t)((nst + 255) / 256)), dim3(256), 0, stream,
+                       ctrl, bend, lo, sbend, sB, L, K, R, nserial);
     hipLaunchKernelGGL(serial_walk_finish_kernel, dim3(1), dim3(256), 0, stream, ctrl, table, M, V, npix,
-                       spp ? spp : 1u, win, bend, path, states, path ? fin : nullptr, lo, L, K, R, depth,
-                       nserial, z, sfloor);
+                       spp ? spp : 1u, win, bend, path, states, path ? fin : nullptr, lo, sbend, sB, L, K, R,
+                       depth, nserial, z, sfloor);
     if (path)
         hipLaunchKernelGGL(serial_states_kernel, dim3((L + 255) / 256), dim3(256), 0, stream, fin, path, win,
                            states, R);

@@ -54,7 +54,7 @@ DeviceState::~DeviceState() {
                     sph_shade, sph_kind, tbvh_nodes, tbvh_tris, tbvh_loose,
                     cam_nodes, cam_tris, ptl_off, ptl_items, spl, tile, gath,
                     sstates, stab, sscan, swin, sjump, sctrl, sbend, spath, sfin,
-                    gspl, gspl_rects, gspl_flag, scheck, slo};
+                    gspl, gspl_rects, gspl_flag, scheck, slo, ssbend, ssb};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
     for (hipEvent_t e : ev)
@@ -910,7 +910,9 @@ static int serial_find_states(WorldState &w, const CameraModel &cam, size_t widt
         }
         HIP_TRY(grow(d->swin, d->swin_cap, wlen));
         HIP_TRY(grow(d->slo, d->slo_cap, L));
-        HIP_TRY(grow(d->sbend, d->sbend_cap, (L + R_walk - 1) / R_walk * K + 4));  // (+4: the chain's 16-B loads)
+        HIP_TRY(grow(d->sbend, d->sbend_cap, (L + R_walk - 1) / R_walk * K));
+        HIP_TRY(grow(d->ssb, d->ssb_cap, (L + R_walk - 1) / R_walk * K));
+        HIP_TRY(grow(d->ssbend, d->ssbend_cap, serial_super_words((uint32_t)L, (uint32_t)K)));
         // recorded block paths: the states of resolved samples become a gather
         const bool gather = env_u64("RT_AMD_SERIAL_GATHER", 1) != 0;
         if (gather) {
@@ -954,7 +956,8 @@ static int serial_find_states(WorldState &w, const CameraModel &cam, size_t widt
                 HIP_TRY(launch_serial_walk(d->sctrl, d->samples, pred, adapt ? Vdev : nullptr,
                                            (uint32_t)npix, (uint32_t)spp, (float)z, (float)serial_floor(spp * R),
                                            d->swin, d->sstates, d->sbend, gather ? d->spath : nullptr,
-                                           gather ? d->sfin : nullptr, d->slo, (uint32_t)L, (uint32_t)K, depth,
+                                           gather ? d->sfin : nullptr, d->slo, d->ssbend, d->ssb, (uint32_t)L,
+                                           (uint32_t)K, depth,
                                            (uint32_t)N, s));
             }
             const auto t1 = std::chrono::steady_clock::now();

@@ -73,6 +73,8 @@ struct DeviceState {
     double *stab = nullptr;          size_t stab_cap = 0;   // prediction tables (render.h serial_tab_doubles)
     double *sscan = nullptr;         size_t sscan_cap = 0;  // their scan's scratch
     uint32_t *slo = nullptr;         size_t slo_cap = 0;    // an iteration's window bases (launch_serial_window)
+    uint32_t *ssbend = nullptr;      size_t ssbend_cap = 0; // superblock ends and block starts (launch_serial_walk)
+    uint32_t *ssb = nullptr;         size_t ssb_cap = 0;
     uint32_t *swin = nullptr;        size_t swin_cap = 0;
     uint32_t *sbend = nullptr;       size_t sbend_cap = 0;
     uint32_t *spath = nullptr;       size_t spath_cap = 0;  // block walks' paths (L x K)
