@@ -210,13 +210,13 @@ uint32_t serial_walk_block(uint32_t L);
 // V (optional): the per-sample scatter-count variances as npix + 1 per-pixel
 // prefix sums of spp var followed by npix per-pixel variances; with it
 // the walk sets the next iteration's candidates per sample in ctrl[5] (<= K):
-// 2 z (sqrt(V over its L samples) + sfloor sqrt(L)) + 2 depth + 2; the count
+// 2 z (sqrt(V over Lw samples) + sfloor sqrt(Lw)) + 2 depth + 2; the count
 // pass and the walks use ctrl[5] when it is set.
 hipError_t launch_serial_walk(uint32_t *ctrl, const float *table, SerialPred M, const double *V,
                               uint32_t npix, uint32_t spp, float z, float sfloor, const uint32_t *win,
                               uint32_t *states, uint32_t *bend, uint32_t *path, uint32_t *fin,
-                              const uint32_t *lo, uint32_t *sbend, uint32_t *sB, uint32_t L, uint32_t K,
-                              uint32_t depth, uint32_t nserial, hipStream_t stream);
+                              const uint32_t *lo, uint32_t *sbend, uint32_t *sB, uint32_t L, uint32_t Lw,
+                              uint32_t K, uint32_t depth, uint32_t nserial, hipStream_t stream);
 // (lo: required; sbend, sB: scratch of serial_super_words(L, K) and ceil(L / R) K
 // u32 for the superblock chain)
 uint32_t serial_super_words(uint32_t L, uint32_t K);

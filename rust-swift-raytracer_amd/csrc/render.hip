@@ -1584,7 +1584,7 @@ __global__ __launch_bounds__(256) void serial_walk_finish_kernel(
     const double *__restrict__ V, uint32_t npix, uint32_t spp, const uint32_t *__restrict__ win,
     const uint32_t *__restrict__ bend, const uint32_t *__restrict__ path, uint32_t *__restrict__ states,
     uint32_t *__restrict__ fin, const uint32_t *__restrict__ lo, const uint32_t *__restrict__ sbend,
-    const uint32_t *__restrict__ sB, uint32_t L, uint32_t Kmax, uint32_t R, uint32_t depth,
+    const uint32_t *__restrict__ sB, uint32_t L, uint32_t Lw, uint32_t Kmax, uint32_t R, uint32_t depth,
     uint32_t nserial, float z, float sfloor) {
     __shared__ uint32_t bstart[256];
     __shared__ uint32_t blo[256];
@@ -1694,7 +1694,7 @@ __global__ __launch_bounds__(256) void serial_walk_finish_kernel(
                 const uint32_t q = min(j / spp, npix);
                 return q < npix ? V[q] + (double)(j - q * spp) * V[npix + 1 + q] : V[npix];
             };
-            const uint32_t a2 = min(a + done, nserial), e = min(a2 + L, nserial);
+            const uint32_t a2 = min(a + done, nserial), e = min(a2 + Lw, nserial);
             const double v = vsum(e) - vsum(a2);
             const double w = ceil(2.0 * (double)z * (sqrt(v > 0.0 ? v : 0.0) + (double)sfloor * sqrt((double)(e - a2)))) +
                              (double)(2u * depth + 2u);
@@ -1954,8 +1954,8 @@ uint32_t serial_walk_block(uint32_t L) {
 hipError_t launch_serial_walk(uint32_t *ctrl, const float *table, SerialPred M, const double *V,
                               uint32_t npix, uint32_t spp, float z, float sfloor, const uint32_t *win,
                               uint32_t *states, uint32_t *bend, uint32_t *path, uint32_t *fin,
-                              const uint32_t *lo, uint32_t *sbend, uint32_t *sB, uint32_t L, uint32_t K,
-                              uint32_t depth, uint32_t nserial, hipStream_t stream) {
+                              const uint32_t *lo, uint32_t *sbend, uint32_t *sB, uint32_t L, uint32_t Lw,
+                              uint32_t K, uint32_t depth, uint32_t nserial, hipStream_t stream) {
     if (!L) return hipSuccess;
     const uint32_t R = serial_walk_block(L);
     const uint32_t nb = (L + R - 1) / R;
@@ -1967,8 +1967,8 @@ hipError_t launch_serial_walk(uint32_t *ctrl, const float *table, SerialPred M, 
     hipLaunchKernelGGL(serial_walk_super_kernel, dim3((uint32_t)((nst + 255) / 256)), dim3(256), 0, stream,
                        ctrl, bend, lo, sbend, sB, L, K, R, nserial);
     hipLaunchKernelGGL(serial_walk_finish_kernel, dim3(1), dim3(256), 0, stream, ctrl, table, M, V, npix,
-                       spp ? spp : 1u, win, bend, path, states, path ? fin : nullptr, lo, sbend, sB, L, K, R,
-                       depth, nserial, z, sfloor);
+                       spp ? spp : 1u, win, bend, path, states, path ? fin : nullptr, lo, sbend, sB, L, Lw, K,
+                       R, depth, nserial, z, sfloor);
     if (path)
         hipLaunchKernelGGL(serial_states_kernel, dim3((L + 255) / 256), dim3(256), 0, stream, fin, path, win,
                            states, R);

@@ -834,7 +834,10 @@ static int serial_find_states(WorldState &w, const CameraModel &cam, size_t widt
         const uint64_t npix = (uint64_t)width * height;
         const double per = (double)(spp * R);
         const uint64_t L = std::max<uint64_t>(1, std::min<uint64_t>(env_u64("RT_AMD_SERIAL_CHUNK", 16384), N));
-        const uint64_t n0 = std::min(N, L);
+        // windows are sized for the deviation over Lw samples (default L; a
+        // longer Lw widens them, a shorter iteration stops less often)
+        const uint64_t Lw = std::max<uint64_t>(1, env_u64("RT_AMD_SERIAL_WLEN", L));
+        const uint64_t n0 = std::min(N, Lw);
         HIP_TRY(grow(d->stab, d->stab_cap, serial_tab_doubles((uint32_t)npix)));
         HIP_TRY(grow(d->sscan, d->sscan_cap, serial_scan_scratch((uint32_t)npix)));
         double *const sums = d->stab + 5 * npix + 2;  // {sum ss, dmax, V(n0), lost count}
@@ -880,7 +883,7 @@ static int serial_find_states(WorldState &w, const CameraModel &cam, size_t widt
         // 72 / 6 / 64; z 1.0 / 1.5 / 2.0 within 5 %: short iterations pay the
         // launch tail, long ones the sqrt(L) wider windows)
         const double z = (double)env_u64("RT_AMD_SERIAL_Z10", 15) / 10.0;
-        const double spread = std::sqrt((double)L * (1.0 + 1.0 / (double)(spp * R)));
+        const double spread = std::sqrt((double)Lw * (1.0 + 1.0 / (double)(spp * R)));
         uint64_t K = (uint64_t)std::ceil(2.0 * z * sigma * spread) + 2 * (uint64_t)depth + 2;
         if (const uint64_t k = env_u64("RT_AMD_SERIAL_K", 0)) K = k;  // (tests: narrow windows)
         // sample a + 1's window must hold every b of sample a: K >= 2 depth + 2
@@ -957,7 +960,7 @@ static int serial_find_states(WorldState &w, const CameraModel &cam, size_t widt
                                            (uint32_t)npix, (uint32_t)spp, (float)z, (float)serial_floor(spp * R),
                                            d->swin, d->sstates, d->sbend, gather ? d->spath : nullptr,
                                            gather ? d->sfin : nullptr, d->slo, d->ssbend, d->ssb, (uint32_t)L,
-                                           (uint32_t)K, depth,
+                                           (uint32_t)Lw, (uint32_t)K, depth,
                                            (uint32_t)N, s));
             }
             const auto t1 = std::chrono::steady_clock::now();
