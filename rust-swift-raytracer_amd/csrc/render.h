@@ -18,7 +18,9 @@ enum : uint32_t { kRngCounter = 1, kRngReplay = 2 };
 //   kRngSerialCheck: one variant; start state win[j] (the found start states),
 //     stores 1 when the sample's end state is not win[j + 1] (p.seed: the
 //     stream state after the frame's last sample), else 0
-enum : uint32_t { kRngSerialCount = 3, kRngSerialEstimate = 4, kRngSerialCheck = 5 };
+//   kRngSerialCoalesce: not a trace_kernel pass -- render_frame launches the
+//     coalescing block search (launch_serial_coalesce) with the frame's scene
+enum : uint32_t { kRngSerialCount = 3, kRngSerialEstimate = 4, kRngSerialCheck = 5, kRngSerialCoalesce = 6 };
 enum : uint32_t { kMatDiffuse = 0, kMatMetal = 1, kMatDielectric = 2, kMatEmission = 3 };
 constexpr uint32_t kPrimaryTriStripW = 8;  // bvh.h kTriStripW
 #ifndef RT_TRACE_RING
@@ -197,15 +199,29 @@ size_t serial_scan_scratch(uint32_t npix);
 hipError_t launch_serial_window(const uint32_t *ctrl, const uint32_t *jump, uint32_t *win, uint32_t n,
                                 SerialPred M, uint32_t *lo, uint32_t L, uint32_t K, uint32_t depth,
                                 uint32_t nserial, hipStream_t stream);
+// Coalescing block search (render.hip serial_coalesce_kernel): one workgroup
+// per block of R samples of the iteration writes bend and path (layouts of
+// launch_serial_walk's block walks) by tracing each block's distinct live
+// offsets once per sample, from win and lo (p.win, p.slo, p.ctrl set as for a
+// count pass; K + depth + 1 < 65535).  tree_lds: stage the sphere tree in LDS
+// (serial_coalesce_lds bytes per workgroup, tree included).
+// dbg (optional, 4 u64, diagnostics): += live offsets traced, trace passes per
+// thread, blocks, the count pass's traces (K x samples) of every block
+hipError_t launch_serial_coalesce(const TraceParams &p, uint32_t *path, uint32_t *bend, uint32_t L, uint32_t Kmax,
+                                  uint32_t R, bool tree_lds, unsigned long long *dbg, hipStream_t stream);
+size_t serial_coalesce_lds(const TraceParams &p, uint32_t K, bool tree_lds);
 // Walk: from sample a = ctrl[4], follows the true path through the candidate
 // table (b of chunk sample jl at candidate k = table[jl * K + k], plane 0 of
 // the slab) as far as it stays inside the candidate windows (at least one
 // sample), writes those samples' start states to states[a + jl] and advances
 // ctrl (a, the state at a, resolved).  bend: scratch of
-// ceil(L / serial_walk_block(L)) * K u32.
+// ceil(L / R) * K u32, R = the block length (serial_walk_block(L) for the
+// count pass; table == nullptr: bend and path were written by the coalescing
+// search, the block walks are skipped).
 uint32_t serial_walk_block(uint32_t L);
+constexpr uint32_t kMaxWalkBlocks = 4096;  // blocks per iteration (the finish kernel's LDS)
 // path, fin (optional, both or neither): scratch of ceil(L / R) R K u32 for the
-// block walks' recorded paths and 4 + 256 u32 for the chain's result; with
+// block walks' recorded paths and 4 + kMaxWalkBlocks u32 for the chain's result; with
 // them the full blocks' states are gathered by a parallel kernel, not re-walked.
 // V (optional): the per-sample scatter-count variances as npix + 1 per-pixel
 // prefix sums of spp var followed by npix per-pixel variances; with it
@@ -216,10 +232,10 @@ hipError_t launch_serial_walk(uint32_t *ctrl, const float *table, SerialPred M, 
                               uint32_t npix, uint32_t spp, float z, float sfloor, const uint32_t *win,
                               uint32_t *states, uint32_t *bend, uint32_t *path, uint32_t *fin,
                               const uint32_t *lo, uint32_t *sbend, uint32_t *sB, uint32_t L, uint32_t Lw,
-                              uint32_t K, uint32_t depth, uint32_t nserial, hipStream_t stream);
-// (lo: required; sbend, sB: scratch of serial_super_words(L, K) and ceil(L / R) K
+                              uint32_t K, uint32_t R, uint32_t depth, uint32_t nserial, hipStream_t stream);
+// (lo: required; sbend, sB: scratch of serial_super_words(L, K, R) and ceil(L / R) K
 // u32 for the superblock chain)
-uint32_t serial_super_words(uint32_t L, uint32_t K);
+uint32_t serial_super_words(uint32_t L, uint32_t K, uint32_t R);
 // inv_spp = 1.0 / (spp as f32) computed from the signed spp (common.rs:345).
 hipError_t launch_resolve_ex(const float *samples, uint32_t *out, uint32_t npix, uint32_t spp,
                              float inv_spp, uint32_t width, uint32_t slab_row0,

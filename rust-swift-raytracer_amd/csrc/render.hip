@@ -656,6 +656,61 @@ __device__ __forceinline__ void resolve_chunk(const TraceParams &p, const float 
     }
 }
 
+// The sphere tree's view for a kernel; kLds: copied into the workgroup's LDS
+// (one barrier).  Returns the walk's first node (its LDS address with kLds).
+// LDS layout: node records (48 B: box float4 x 2 | 8 x u16 links) | prims
+// (float4) | shade (2 x float4 / sphere) | ids (u32) | kinds (u32), at the
+// start of the dynamic LDS (trace_lds_bytes).  Node references become record
+// LDS addresses (base + index * 48; the kernels have no static LDS before it,
+// so base is 0 and they stay below 65520: the copy holds < 1366 nodes); 0xFFFF
+// stays the end marker.
+template <bool kLds>
+__device__ __forceinline__ uint32_t stage_tree(const TraceParams &p, float4 *lds, BvhView &view) {
+    if (!kLds) {
+        view = BvhView{p.bvh_nodes, p.bvh_miss, nullptr, p.bvh_prims, p.bvh_prim_id,
+                       p.sph_shade, p.sph_kind};
+        return 0;
+    }
+    float4 *n4 = lds;
+    const uint32_t lbase = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) float4 *)lds;
+    float4 *p4 = n4 + 3 * p.nnodes;
+    float4 *s4 = p4 + p.nprims;
+    uint32_t *id = reinterpret_cast<uint32_t *>(s4 + 2 * p.nsph_padded);
+    uint32_t *kd = id + p.nprims;
+    const uint16_t *g16 = p.bvh_miss16;
+    for (uint32_t i = threadIdx.x; i < p.nnodes; i += blockDim.x) {
+        float4 b0 = p.bvh_nodes[2 * i];
+        const uint32_t a = __float_as_uint(b0.w);
+        float4 b1 = p.bvh_nodes[2 * i + 1];
+        if (!(a & kLeafBitDev)) {
+            b0.w = __uint_as_float(lbase + a * 48u);                 // left child's record
+            b1.w = __uint_as_float(8u * __float_as_uint(b1.w));      // split axis * 8
+        }
+        n4[3 * i] = b0;
+        n4[3 * i + 1] = b1;
+        uint32_t w[4];
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t l0 = g16[8 * i + 2 * k], l1 = g16[8 * i + 2 * k + 1];
+            w[k] = (l0 == 0xFFFFu ? 0xFFFFu : lbase + l0 * 48u) |
+                   ((l1 == 0xFFFFu ? 0xFFFFu : lbase + l1 * 48u) << 16);
+        }
+        n4[3 * i + 2] = make_float4(__uint_as_float(w[0]), __uint_as_float(w[1]),
+                                    __uint_as_float(w[2]), __uint_as_float(w[3]));
+    }
+    for (uint32_t i = threadIdx.x; i < p.nprims; i += blockDim.x) {
+        p4[i] = p.bvh_prims[i];
+        id[i] = p.bvh_prim_id[i];
+    }
+    for (uint32_t i = threadIdx.x; i < p.nsph_padded; i += blockDim.x) {
+        s4[2 * i] = p.sph_shade[2 * i];
+        s4[2 * i + 1] = p.sph_shade[2 * i + 1];
+        kd[i] = p.sph_kind[i];
+    }
+    __syncthreads();
+    view = BvhView{n4, nullptr, nullptr, p4, id, s4, kd};
+    return lbase;
+}
+
 // ------------------------------------------------------------ trace kernel
 // kBvh: sphere search through the exact BVH (else brute force).  kLds: the
 // tree is copied into the workgroup's LDS once (persistent grid), so every
@@ -717,55 +772,7 @@ void trace_kernel(TraceParams p) {
     const uint32_t lane = __lane_id();
     extern __shared__ float4 lds[];
     BvhView view;
-    uint32_t sph_root = 0;  // the sphere walk's first node (its LDS address with kLds)
-    if (kLds) {
-        // layout: node records (48 B: box float4 x 2 | 8 x u16 links) | prims
-        // (float4) | shade (2 x float4 / sphere) | ids (u32) | kinds (u32).
-        // Node references become record LDS addresses (base + index * 48; the
-        // kernel has no static LDS, so base is 0 and they stay below 65520: the
-        // copy holds < 1366 nodes); 0xFFFF stays the end marker.
-        float4 *n4 = lds;
-        const uint32_t lbase = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) float4 *)lds;
-        sph_root = lbase;
-        float4 *p4 = n4 + 3 * p.nnodes;
-        float4 *s4 = p4 + p.nprims;
-        uint32_t *id = reinterpret_cast<uint32_t *>(s4 + 2 * p.nsph_padded);
-        uint32_t *kd = id + p.nprims;
-        const uint16_t *g16 = p.bvh_miss16;
-        for (uint32_t i = threadIdx.x; i < p.nnodes; i += blockDim.x) {
-            float4 b0 = p.bvh_nodes[2 * i];
-            const uint32_t a = __float_as_uint(b0.w);
-            float4 b1 = p.bvh_nodes[2 * i + 1];
-            if (!(a & kLeafBitDev)) {
-                b0.w = __uint_as_float(lbase + a * 48u);                 // left child's record
-                b1.w = __uint_as_float(8u * __float_as_uint(b1.w));      // split axis * 8
-            }
-            n4[3 * i] = b0;
-            n4[3 * i + 1] = b1;
-            uint32_t w[4];
-            for (int k = 0; k < 4; ++k) {
-                const uint32_t l0 = g16[8 * i + 2 * k], l1 = g16[8 * i + 2 * k + 1];
-                w[k] = (l0 == 0xFFFFu ? 0xFFFFu : lbase + l0 * 48u) |
-                       ((l1 == 0xFFFFu ? 0xFFFFu : lbase + l1 * 48u) << 16);
-            }
-            n4[3 * i + 2] = make_float4(__uint_as_float(w[0]), __uint_as_float(w[1]),
-                                        __uint_as_float(w[2]), __uint_as_float(w[3]));
-        }
-        for (uint32_t i = threadIdx.x; i < p.nprims; i += blockDim.x) {
-            p4[i] = p.bvh_prims[i];
-            id[i] = p.bvh_prim_id[i];
-        }
-        for (uint32_t i = threadIdx.x; i < p.nsph_padded; i += blockDim.x) {
-            s4[2 * i] = p.sph_shade[2 * i];
-            s4[2 * i + 1] = p.sph_shade[2 * i + 1];
-            kd[i] = p.sph_kind[i];
-        }
-        __syncthreads();
-        view = BvhView{n4, nullptr, nullptr, p4, id, s4, kd};
-    } else {
-        view = BvhView{p.bvh_nodes, p.bvh_miss, nullptr, p.bvh_prims, p.bvh_prim_id,
-                       p.sph_shade, p.sph_kind};
-    }
+    const uint32_t sph_root = stage_tree<kLds>(p, lds, view);  // the sphere walk's first node
 
     F3 org = f3(0, 0, 0), dir = f3(0, 0, 0), inv = f3(0, 0, 0);
     float thr_r = 1.0f, thr_g = 1.0f, thr_b = 1.0f;  // ray_color's final_color
@@ -1586,10 +1593,10 @@ __global__ __launch_bounds__(256) void serial_walk_finish_kernel(
     uint32_t *__restrict__ fin, const uint32_t *__restrict__ lo, const uint32_t *__restrict__ sbend,
     const uint32_t *__restrict__ sB, uint32_t L, uint32_t Lw, uint32_t Kmax, uint32_t R, uint32_t depth,
     uint32_t nserial, float z, float sfloor) {
-    __shared__ uint32_t bstart[256];
-    __shared__ uint32_t blo[256];
+    __shared__ uint32_t bstart[kMaxWalkBlocks];
+    __shared__ uint32_t blo[kMaxWalkBlocks];
     __shared__ uint32_t nfull;
-    __shared__ uint32_t scol[256 / kSuperBlocks + 1];  // the chain's column in each superblock
+    __shared__ uint32_t scol[kMaxWalkBlocks / kSuperBlocks + 1];  // the chain's column in each superblock
     __shared__ uint32_t cB, cblk, cleft;
     if (ctrl[0] != 0u) {
         if (fin && threadIdx.x == 0) fin[1] = 0u;  // (serial_states_kernel: nothing)
@@ -1726,6 +1733,322 @@ __global__ __launch_bounds__(256) void serial_states_kernel(const uint32_t *__re
     const uint32_t blk = jl / R;
     const uint32_t B = path[(size_t)(jl - blk * R) * fin[2] + fin[4 + blk]];
     states[fin[0] + jl] = win[2u * jl + 3u * B];
+}
+
+// ---- coalescing block search (kRngSerialCoalesce)
+// The count pass traces every (sample, candidate) pair of an iteration (L K
+// traces), yet the candidate paths of a block coalesce: two candidates whose
+// offsets meet at some sample share every later step, and in a random walk
+// with per-sample variance s^2 only about K / sqrt(pi s^2 n) of K neighbouring
+// starts are still distinct after n samples.  Here one workgroup owns one
+// block of R samples: it keeps the block's distinct live offsets (sorted, in
+// LDS) and the live slot of each of the K candidates of the block's first
+// sample, traces each live offset once per sample, and merges equal offsets.
+// It writes what serial_walk_blocks_kernel derives from the count table --
+// bend (the block end of every candidate, or kWalkLeft | the samples walked)
+// and path (the offset of every candidate at every sample) -- so the
+// superblock, finish and gather kernels run unchanged.
+
+// One sample of the reference's ray_color (common.rs:263-285) from stream
+// state rng, for frame sample j: the number of diffuse/metal scatters b (the
+// sample draws 2 + 3b numbers, common.rs:335-336 and 32-38).  The same helper
+// arithmetic as trace_kernel's lane state machine, without colours: whole
+// walks, the static triangle tree at every bounce (the camera tree and the
+// primary lists are exact shortcuts of it), no sphere lists.
+template <bool kBvh, bool kLds, int kMesh>
+__device__ __forceinline__ uint32_t serial_trace_b(const TraceParams &p, const BvhView &view, uint32_t sph_root,
+                                                uint32_t rng, uint32_t j) {
+    const uint32_t pix = fdiv(j, p.div_sspp);
+    const uint32_t row = fdiv(pix, p.div_width);
+    const uint32_t col = pix - row * p.width;
+    const float un = (float)col + draw01(rng);  // camera.rs:84-89 via common.rs:335-337
+    const float vn = (float)row + draw01(rng);
+#ifndef RT_NO_XDIV
+    const bool xd = p.xdiv_uv != 0;
+#else
+    const bool xd = false;
+#endif
+    const float u = xd ? xdiv(un, p.wden, p.wrcp) : un / p.wden;
+    const float v = xd ? xdiv(vn, p.hden, p.hrcp) : vn / p.hden;
+    const F3 h = f3(p.cam[6], p.cam[7], p.cam[8]);
+    const F3 vv = f3(p.cam[9], p.cam[10], p.cam[11]);
+    F3 org = f3(p.cam[0], p.cam[1], p.cam[2]);
+    const F3 llc = f3(p.cam[3], p.cam[4], p.cam[5]);
+    F3 dir = unit(((llc + scale(h, u)) + scale(vv, v)) - org);
+    uint32_t b = 0, cnt = 0;  // (cnt: the helpers' work counters, unused)
+    for (int32_t bounce = 0; bounce < p.depth; ++bounce) {
+        const F3 inv = f3(slab_rcp(dir.x), slab_rcp(dir.y), slab_rcp(dir.z));
+        const uint32_t oct = (inv.x < 0.0f ? 1u : 0u) | (inv.y < 0.0f ? 2u : 0u) | (inv.z < 0.0f ? 4u : 0u);
+        float best_t = __builtin_inff();
+        int best_i = -1;
+        if (kBvh) {  // World::hit (common.rs:241-247) through the exact tree
+            spheres_big(p, org, dir, best_t, best_i);
+            constexpr uint32_t kEnd = kLds ? 0xFFFFu : kNodeEndDev;
+            const SphBound bnd = sph_bound(p, org);
+            F3 nlo, nhi;
+            sphere_slabs(org, inv, sph_inflation(p, bnd, best_t), nlo, nhi);
+            const uint32_t octm = ((oct & 1u) ? 48u : 0u) | ((oct & 2u) ? 48u << 8 : 0u) |
+                                  ((oct & 4u) ? 48u << 16 : 0u);
+            uint32_t node = sph_root;
+            do {
+                uint32_t leaf;
+                if (sphere_node<kLds>(view, inv, oct, octm, best_t, nlo, nhi, node, leaf, cnt))
+                    sphere_leaf(p, view, org, dir, inv, leaf, best_t, best_i, bnd, nlo, nhi, cnt);
+            } while (node != kEnd);
+        } else {
+            spheres_brute(p, org, dir, best_t, best_i);
+        }
+        float tri_t = __builtin_inff();  // Mesh::hit (common.rs:178-223)
+        int tri_i = -1;
+        if (kMesh == 2) {
+            float e = 0.0f;
+            if (tri_begin(p, org, dir, best_t, false, e, tri_t, tri_i, cnt, cnt)) {
+                const F3 dlt2 = f3(2.0f * (org.x - p.tbvh_oc[0]), 2.0f * (org.y - p.tbvh_oc[1]),
+                                   2.0f * (org.z - p.tbvh_oc[2]));
+                F3 nlo, nhi;
+                sphere_slabs(org, inv, e, nlo, nhi);
+                float cap = fminf(best_t, tri_t);
+                uint32_t node = 0;
+                do {
+                    uint32_t leaf;
+                    if (tri_node(p, nlo, nhi, inv, dlt2, false, cap, node, leaf, cnt)) {
+                        tri_leaf(p, org, dir, false, leaf, best_t, tri_t, tri_i, cnt, cnt);
+                        cap = fminf(best_t, tri_t);
+                    }
+                } while (node != kNodeEndDev);
+            }
+        } else if (kMesh == 1) {
+            triangles_brute(p, org, dir, best_t, tri_t, tri_i, cnt);
+        }
+        if (tri_i < 0 && best_i < 0) return b;  // background (common.rs:276-281): no draws
+        F3 pos, nrm;
+        uint32_t kind;
+        float param;
+        if (tri_i >= 0) {  // a triangle wins a tie against a sphere
+            pos = org + scale(dir, tri_t);
+            const float4 *g = p.tri_geo + 4u * (uint32_t)tri_i;
+            const float4 A = g[0], Nn = g[3];
+            nrm = f3(Nn.x, Nn.y, Nn.z);
+            const float *m = p.mats + 8u * __float_as_uint(A.w);
+            kind = __float_as_uint(m[0]);
+            param = m[4];
+        } else {
+            const float4 S = view.shade[2 * best_i];
+            param = view.shade[2 * best_i + 1].w;
+            kind = view.kinds[best_i];
+            pos = org + scale(dir, best_t);
+            nrm = unit(divide_by(pos - f3(S.x, S.y, S.z), S.w));  // common.rs:95
+        }
+        F3 v = nrm;
+        bool keep_normal = false;
+        if (kind == kMatDiffuse || kind == kMatMetal) {
+            const F3 ru = draw_unit(rng);
+            ++b;
+            if (kind == kMatDiffuse) {  // materials.rs:42-52
+                v = nrm + ru;
+                const float eps = 1e-8f;
+                keep_normal = fabsf(v.x) < eps && fabsf(v.y) < eps && fabsf(v.z) < eps;
+            } else {  // materials.rs:54-63: absorbed when the scatter points inward
+                const F3 refl = dir - scale(nrm, 2.0f * dot(dir, nrm));
+                v = refl + scale(ru, param);
+                if (!(dot(v, nrm) >= 0.0f)) return b;
+            }
+        } else if (kind == kMatDielectric) {  // materials.rs:65-97 (no draws)
+            F3 n2 = nrm;
+            float eta = param;
+            if (dot(dir, nrm) >= 0.0f) { n2 = -nrm; eta = 1.0f / param; }
+            const float cos_t = dot(-dir, n2);
+            const F3 perp = scale(dir + scale(n2, cos_t), eta);
+            const F3 par = scale(n2, -xsqrt(fabsf(1.0f - dot(perp, perp))));
+            v = perp + par;
+        } else {
+            return b;  // Emission (materials.rs:100-102)
+        }
+        org = pos;
+        dir = keep_normal ? nrm : unit(v);
+    }
+    return b;  // depth exhausted (common.rs:284)
+}
+
+// Exclusive prefix sum of one u32 per thread over the 256-thread workgroup
+// (wave scans, then the 4 wave totals); *total gets the sum.  Contains barriers.
+__device__ __forceinline__ uint32_t block_exscan256(uint32_t v, uint32_t *wsum, uint32_t *total) {
+    const uint32_t lane = threadIdx.x & (kWave - 1u), wv = threadIdx.x / kWave;
+    uint32_t x = v;
+#pragma unroll
+    for (uint32_t off = 1; off < kWave; off <<= 1) {
+        const uint32_t y = __shfl_up(x, off);
+        if (lane >= off) x += y;
+    }
+    if (lane == kWave - 1u) wsum[wv] = x;
+    __syncthreads();
+    uint32_t before = 0;
+    for (uint32_t w = 0; w < wv; ++w) before += wsum[w];
+    *total = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+    return before + x - v;
+}
+
+constexpr uint32_t kCoalesceThreads = 256;
+constexpr uint32_t kSlotDead = 0xFFFFFFFFu;
+
+// LDS bytes of the coalescing workgroup after the tree: cand (u16 x K), three
+// u32 lists of Kp = K + depth + 1 live offsets, two bitmaps and a prefix of W
+// words (all 16-B aligned)
+__host__ __device__ inline size_t coalesce_lds_bytes(uint32_t K, uint32_t depth) {
+    const size_t Kp = (size_t)K + depth + 1, W = (Kp + 31) / 32;
+    auto al = [](size_t x) { return (x + 15) & ~(size_t)15; };
+    return al(2 * (size_t)K) + 3 * al(4 * Kp) + 3 * al(4 * W) + 16;
+}
+
+template <bool kBvh, bool kLds, int kMesh>
+__global__ __launch_bounds__(kCoalesceThreads) void serial_coalesce_kernel(TraceParams p, uint32_t *__restrict__ path,
+                                                                           uint32_t *__restrict__ bend, uint32_t L,
+                                                                           uint32_t Kmax, uint32_t R,
+                                                                           uint32_t tree_bytes,
+                                                                           unsigned long long *__restrict__ dbg) {
+    if (p.ctrl[0] != 0u) return;
+    const uint32_t K = serial_k(p.ctrl, Kmax);
+    const uint32_t a = p.ctrl[4];
+    const uint32_t n = min(L, p.nserial - a);
+    const uint32_t nb = (n + R - 1) / R;
+    const uint32_t blk = blockIdx.x;
+    if (blk >= nb) return;  // (whole workgroup, before any barrier)
+    extern __shared__ float4 lds[];
+    BvhView view;
+    const uint32_t sph_root = stage_tree<kLds>(p, lds, view);
+    const uint32_t depth = p.depth > 0 ? (uint32_t)p.depth : 0u;
+    const uint32_t Kp = K + depth + 1, W = (Kp + 31) / 32;
+    auto al = [](uint32_t x) { return (x + 15u) & ~15u; };
+    char *c = reinterpret_cast<char *>(lds) + tree_bytes;
+    uint16_t *cand = reinterpret_cast<uint16_t *>(c);  // live slot of each candidate (0xFFFF: left)
+    c += al(2 * K);
+    uint32_t *LB = reinterpret_cast<uint32_t *>(c);    // live offsets, ascending
+    c += al(4 * Kp);
+    uint32_t *LBn = reinterpret_cast<uint32_t *>(c);   // the next sample's
+    c += al(4 * Kp);
+    uint32_t *NB = reinterpret_cast<uint32_t *>(c);    // each live offset's end (kSlotDead: left)
+    c += al(4 * Kp);
+    uint32_t *bits0 = reinterpret_cast<uint32_t *>(c);  // the ends present, relative to the window
+    c += al(4 * W);
+    uint32_t *bits1 = reinterpret_cast<uint32_t *>(c);
+    c += al(4 * W);
+    uint32_t *wpre = reinterpret_cast<uint32_t *>(c);   // exclusive popcount prefix of the bitmap
+    c += al(4 * W);
+    uint32_t *wsum = reinterpret_cast<uint32_t *>(c);   // block_exscan256's wave totals
+    // (all dynamic: the tree's LDS node addresses assume no static LDS below it)
+    const uint32_t t = threadIdx.x;
+    const uint32_t j0 = blk * R, j1 = min(j0 + R, n);
+    const size_t stride = (size_t)nb * K;
+    const uint32_t base = p.slo[j0];
+    for (uint32_t k = t; k < K; k += kCoalesceThreads) {
+        cand[k] = (uint16_t)k;
+        LB[k] = base + k;
+    }
+    for (uint32_t w = t; w < W; w += kCoalesceThreads) bits0[w] = bits1[w] = 0u;
+    uint32_t nlive = K;
+    uint32_t d_traces = 0, d_passes = 0;  // (dbg: RT_AMD_SERIAL_DEBUG)
+    __syncthreads();
+    for (uint32_t s = 0; j0 + s < j1; ++s) {
+        d_traces += nlive;
+        d_passes += (nlive + kCoalesceThreads - 1) / kCoalesceThreads;
+        const uint32_t jl = j0 + s;
+        const uint32_t l = p.slo[jl];  // the window of sample jl: [l, l + K)
+        uint32_t *bits = (s & 1u) ? bits1 : bits0;
+        uint32_t *bnext = (s & 1u) ? bits0 : bits1;
+        // every distinct live offset once: its sample's end offset
+        for (uint32_t i = t; i < nlive; i += kCoalesceThreads) {
+            const uint32_t B = LB[i];
+            uint32_t e = kSlotDead;
+            if (B >= l && B - l < K) {
+                e = B + serial_trace_b<kBvh, kLds, kMesh>(p, view, sph_root, p.win[2u * jl + 3u * B], a + jl);
+                const uint32_t r = e - l;  // < K + depth
+                atomicOr(&bits[r >> 5], 1u << (r & 31u));
+            }
+            NB[i] = e;
+        }
+        __syncthreads();
+        // ranks of the distinct ends: popcount prefix over the bitmap words
+        const uint32_t per = (W + kCoalesceThreads - 1) / kCoalesceThreads;
+        const uint32_t w0 = min(t * per, W), w1 = min(w0 + per, W);
+        uint32_t cntw = 0;
+        for (uint32_t w = w0; w < w1; ++w) cntw += __popc(bits[w]);
+        uint32_t total = 0;
+        uint32_t run = block_exscan256(cntw, wsum, &total);
+        for (uint32_t w = w0; w < w1; ++w) {
+            wpre[w] = run;
+            run += __popc(bits[w]);
+        }
+        __syncthreads();
+        auto rank = [&](uint32_t e) {
+            const uint32_t r = e - l;
+            return wpre[r >> 5] + __popc(bits[r >> 5] & ((1u << (r & 31u)) - 1u));
+        };
+        for (uint32_t i = t; i < nlive; i += kCoalesceThreads) {
+            const uint32_t e = NB[i];
+            if (e != kSlotDead) LBn[rank(e)] = e;  // (merged slots write the same value)
+        }
+        for (uint32_t k = t; k < K; k += kCoalesceThreads) {
+            const uint32_t sl = cand[k];
+            if (sl == 0xFFFFu) continue;
+            path[(size_t)s * stride + (size_t)blk * K + k] = LB[sl];
+            const uint32_t e = NB[sl];
+            if (e == kSlotDead) {
+                cand[k] = 0xFFFFu;
+                bend[(size_t)blk * K + k] = kWalkLeft | s;
+            } else {
+                cand[k] = (uint16_t)rank(e);
+            }
+        }
+        for (uint32_t w = t; w < W; w += kCoalesceThreads) bnext[w] = 0u;
+        nlive = total;
+        uint32_t *sw = LB;
+        LB = LBn;
+        LBn = sw;
+        __syncthreads();
+    }
+    for (uint32_t k = t; k < K; k += kCoalesceThreads) {
+        const uint32_t sl = cand[k];
+        if (sl != 0xFFFFu) bend[(size_t)blk * K + k] = LB[sl];
+    }
+    if (dbg != nullptr && t == 0) {
+        atomicAdd(dbg, (unsigned long long)d_traces);
+        atomicAdd(dbg + 1, (unsigned long long)d_passes);
+        atomicAdd(dbg + 2, 1ull);
+        atomicAdd(dbg + 3, (unsigned long long)K * (j1 - j0));
+    }
+}
+
+template <bool kBvh, bool kLds>
+static void launch_coalesce_m(const TraceParams &p, uint32_t *path, uint32_t *bend, uint32_t L, uint32_t Kmax,
+                              uint32_t R, size_t tree_bytes, size_t lds, unsigned long long *dbg,
+                              hipStream_t stream) {
+    const uint32_t nb = (L + R - 1) / R;
+    const int mesh = trace_mesh_kind(p.ntri != 0, p.tnodes != 0);
+    if (mesh == 2)
+        hipLaunchKernelGGL((serial_coalesce_kernel<kBvh, kLds, 2>), dim3(nb), dim3(kCoalesceThreads), lds, stream, p,
+                           path, bend, L, Kmax, R, (uint32_t)tree_bytes, dbg);
+    else if (mesh == 1)
+        hipLaunchKernelGGL((serial_coalesce_kernel<kBvh, kLds, 1>), dim3(nb), dim3(kCoalesceThreads), lds, stream, p,
+                           path, bend, L, Kmax, R, (uint32_t)tree_bytes, dbg);
+    else
+        hipLaunchKernelGGL((serial_coalesce_kernel<kBvh, kLds, 0>), dim3(nb), dim3(kCoalesceThreads), lds, stream, p,
+                           path, bend, L, Kmax, R, (uint32_t)tree_bytes, dbg);
+}
+
+size_t serial_coalesce_lds(const TraceParams &p, uint32_t K, bool tree_lds) {
+    const size_t tb = tree_lds ? (trace_lds_bytes(p) + 15) & ~(size_t)15 : 0;
+    return tb + coalesce_lds_bytes(K, p.depth > 0 ? (uint32_t)p.depth : 0u);
+}
+
+hipError_t launch_serial_coalesce(const TraceParams &p, uint32_t *path, uint32_t *bend, uint32_t L, uint32_t Kmax,
+                                  uint32_t R, bool tree_lds, unsigned long long *dbg, hipStream_t stream) {
+    if (!L || !R) return hipSuccess;
+    const size_t tb = tree_lds ? (trace_lds_bytes(p) + 15) & ~(size_t)15 : 0;
+    const size_t lds = serial_coalesce_lds(p, Kmax, tree_lds);
+    if (p.nnodes && tree_lds) launch_coalesce_m<true, true>(p, path, bend, L, Kmax, R, tb, lds, dbg, stream);
+    else if (p.nnodes) launch_coalesce_m<true, false>(p, path, bend, L, Kmax, R, tb, lds, dbg, stream);
+    else launch_coalesce_m<false, false>(p, path, bend, L, Kmax, R, tb, lds, dbg, stream);
+    return hipGetLastError();
 }
 
 // ---- the estimate reduction (render.h serial_tab_doubles for the layout)
@@ -1941,8 +2264,8 @@ hipError_t launch_serial_window(const uint32_t *ctrl, const uint32_t *jump, uint
     return hipGetLastError();
 }
 
-uint32_t serial_super_words(uint32_t L, uint32_t K) {
-    const uint32_t nb = (L + serial_walk_block(L) - 1) / serial_walk_block(L);
+uint32_t serial_super_words(uint32_t L, uint32_t K, uint32_t R) {
+    const uint32_t nb = (L + R - 1) / R;
     return (nb + kSuperBlocks - 1) / kSuperBlocks * K;
 }
 
@@ -1955,15 +2278,17 @@ hipError_t launch_serial_walk(uint32_t *ctrl, const float *table, SerialPred M, 
                               uint32_t npix, uint32_t spp, float z, float sfloor, const uint32_t *win,
                               uint32_t *states, uint32_t *bend, uint32_t *path, uint32_t *fin,
                               const uint32_t *lo, uint32_t *sbend, uint32_t *sB, uint32_t L, uint32_t Lw,
-                              uint32_t K, uint32_t depth, uint32_t nserial, hipStream_t stream) {
-    if (!L) return hipSuccess;
-    const uint32_t R = serial_walk_block(L);
+                              uint32_t K, uint32_t R, uint32_t depth, uint32_t nserial, hipStream_t stream) {
+    if (!L || !R) return hipSuccess;
     const uint32_t nb = (L + R - 1) / R;
+    if (nb > kMaxWalkBlocks) return hipErrorInvalidValue;
     const uint64_t nt = (uint64_t)nb * K;
     const uint64_t nst = (uint64_t)((nb + kSuperBlocks - 1) / kSuperBlocks) * K;
     if (!fin) path = nullptr;
-    hipLaunchKernelGGL(serial_walk_blocks_kernel, dim3((uint32_t)((nt + 255) / 256)), dim3(256), 0, stream,
-                       ctrl, table, M, bend, path, lo, L, K, R, depth, nserial);
+    if (table == nullptr && !path) return hipErrorInvalidValue;  // (the coalescing search needs the gather)
+    if (table != nullptr)
+        hipLaunchKernelGGL(serial_walk_blocks_kernel, dim3((uint32_t)((nt + 255) / 256)), dim3(256), 0, stream,
+                           ctrl, table, M, bend, path, lo, L, K, R, depth, nserial);
     hipLaunchKernelGGL(serial_walk_super_kernel, dim3((uint32_t)((nst + 255) / 256)), dim3(256), 0, stream,
                        ctrl, bend, lo, sbend, sB, L, K, R, nserial);
     hipLaunchKernelGGL(serial_walk_finish_kernel, dim3(1), dim3(256), 0, stream, ctrl, table, M, V, npix,

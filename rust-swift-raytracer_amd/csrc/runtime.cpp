@@ -580,7 +580,7 @@ int render_frame(WorldState &w, const CameraModel &cam, size_t width, size_t hei
         const uint64_t njobs = (uint64_t)sp->nsamples * sp->variants;
         if (njobs == 0) return 0;
         if (njobs > 0x7FFFFFFFull) { set_error("serial pass too large"); return -1; }
-        HIP_TRY(grow(d->samples, d->samples_cap, 3 * njobs));
+        if (sp->mode != kRngSerialCoalesce) HIP_TRY(grow(d->samples, d->samples_cap, 3 * njobs));
         p.samples = d->samples;
         p.ring = nullptr;
         p.ring_shift = 0;
@@ -614,8 +614,16 @@ int render_frame(WorldState &w, const CameraModel &cam, size_t width, size_t hei
             1, std::min<uint64_t>({(uint64_t)(p.step ? 64 : 16), kMaxParts, njobs / (16 * chunk) + 1}));
         if (const uint64_t np = env_u64("RT_AMD_SERIAL_PARTS", 0)) parts = std::min<uint64_t>(np, kMaxParts);
         p.nparts = (uint32_t)parts;
-        HIP_TRY(hipMemsetAsync(d->counter, 0, parts * 128, s));
-        HIP_TRY(launch_trace(p, (uint32_t)blocks, s));
+        if (sp->mode == kRngSerialCoalesce) {
+            // one workgroup per block of sp->R samples; the tree in LDS when it
+            // fits beside the search's own arrays (64 KB per workgroup)
+            const bool tree_lds = p.use_lds && serial_coalesce_lds(p, sp->variants, true) <= 64 * 1024;
+            HIP_TRY(launch_serial_coalesce(p, sp->path, sp->bend, sp->nsamples, sp->variants, sp->R, tree_lds,
+                                           sp->dbg, s));
+        } else {
+            HIP_TRY(hipMemsetAsync(d->counter, 0, parts * 128, s));
+            HIP_TRY(launch_trace(p, (uint32_t)blocks, s));
+        }
         HIP_TRY(hipEventRecord(d->done, s));
         d->done_stream = s;
         d->last_jobs = 0;  // the slab holds counts now, not samples
@@ -833,7 +841,20 @@ static int serial_find_states(WorldState &w, const CameraModel &cam, size_t widt
             1, std::min<uint64_t>({(est + spp - 1) / spp, 64, 0x7FFFFFFFull / N}));
         const uint64_t npix = (uint64_t)width * height;
         const double per = (double)(spp * R);
-        const uint64_t L = std::max<uint64_t>(1, std::min<uint64_t>(env_u64("RT_AMD_SERIAL_CHUNK", 16384), N));
+        // The coalescing block search (serial_coalesce_kernel) or the count
+        // pass over every (sample, candidate) pair + block walks.  Coalescing
+        // traces 0.33-0.45 of the count pass's traces but runs each block's
+        // samples in sequence: it wins where a trace is short -- brute-force
+        // scenes, i.e. no sphere or triangle tree (< 16 of each: render()'s
+        // scenes; 960x540x16 c_raytracer 338 -> 308 ms, world.txt 301 -> 233
+        // ms) -- and loses on tree walks (RTOW 238 -> 620 ms).
+        // RT_AMD_SERIAL_COALESCE: 0 off, 1 on, unset: that rule.
+        const bool trees = o.accel != RT_ACCEL_BRUTE && (d->nnodes > 0 || d->tnodes > 0);
+        bool coalesce = env_u64("RT_AMD_SERIAL_COALESCE", trees ? 0 : 1) != 0 && depth < 1024;
+        // (iterations of 128 k samples in blocks of 32 for the coalescing search,
+        // profiles/round3_serial/coalesce_sweep*.log; 16 k for the count pass)
+        const uint64_t L = std::max<uint64_t>(
+            1, std::min<uint64_t>(env_u64("RT_AMD_SERIAL_CHUNK", coalesce ? 131072 : 16384), N));
         // windows are sized for the deviation over Lw samples (default L; a
         // longer Lw widens them, a shorter iteration stops less often)
         const uint64_t Lw = std::max<uint64_t>(1, env_u64("RT_AMD_SERIAL_WLEN", L));
@@ -892,6 +913,9 @@ static int serial_find_states(WorldState &w, const CameraModel &cam, size_t widt
             set_error("RT_RNG_SERIAL: candidate table too large");
             return -5;
         }
+        // (the coalescing workgroup keeps K candidates' u16 slots and K + depth
+        // + 1 live offsets in LDS: wider windows take the count pass)
+        if (K > 4096) coalesce = false;
         // The walks size each iteration's windows from the per-pixel variances
         // (V: prefix sums over pixels of spp var, then var; the variance of
         // samples [0, j) is PV[p] + (j - p spp) var[p]): 2 z (sqrt(V) + 0.05
@@ -905,7 +929,13 @@ static int serial_find_states(WorldState &w, const CameraModel &cam, size_t widt
             set_error("RT_RNG_SERIAL: candidate window too large");
             return -5;
         }
-        const uint64_t R_walk = serial_walk_block((uint32_t)L);
+        // block length: the count pass's walks use serial_walk_block(L) (256
+        // blocks); the coalescing search RT_AMD_SERIAL_R samples (default 32,
+        // <= kMaxWalkBlocks blocks per iteration)
+        const uint64_t R_walk =
+            coalesce ? std::min<uint64_t>(L, std::max<uint64_t>({env_u64("RT_AMD_SERIAL_R", 32), 1,
+                                                                 (L + kMaxWalkBlocks - 1) / kMaxWalkBlocks}))
+                     : serial_walk_block((uint32_t)L);
         uint32_t K0 = 0;  // the first iteration's candidates (later ones: the walks)
         if (adapt) {
             const double w0 = 2.0 * z * (std::sqrt(std::max(sm[2], 0.0)) + serial_floor(spp * R) * std::sqrt((double)n0));
@@ -915,12 +945,13 @@ static int serial_find_states(WorldState &w, const CameraModel &cam, size_t widt
         HIP_TRY(grow(d->slo, d->slo_cap, L));
         HIP_TRY(grow(d->sbend, d->sbend_cap, (L + R_walk - 1) / R_walk * K));
         HIP_TRY(grow(d->ssb, d->ssb_cap, (L + R_walk - 1) / R_walk * K));
-        HIP_TRY(grow(d->ssbend, d->ssbend_cap, serial_super_words((uint32_t)L, (uint32_t)K)));
+        HIP_TRY(grow(d->ssbend, d->ssbend_cap, serial_super_words((uint32_t)L, (uint32_t)K, (uint32_t)R_walk)));
         // recorded block paths: the states of resolved samples become a gather
-        const bool gather = env_u64("RT_AMD_SERIAL_GATHER", 1) != 0;
+        // (the coalescing search has no count table to re-walk: always)
+        const bool gather = coalesce || env_u64("RT_AMD_SERIAL_GATHER", 1) != 0;
         if (gather) {
             HIP_TRY(grow(d->spath, d->spath_cap, (L + R_walk - 1) / R_walk * R_walk * K));
-            if (!d->sfin) HIP_TRY(hipMalloc((void **)&d->sfin, (4 + 256) * 4));
+            if (!d->sfin) HIP_TRY(hipMalloc((void **)&d->sfin, (4 + kMaxWalkBlocks) * 4));
         }
         if (!d->sjump) {
             const std::vector<uint32_t> jt = xorshift_jump_table();
@@ -935,9 +966,12 @@ static int serial_find_states(WorldState &w, const CameraModel &cam, size_t widt
         uint32_t ctrl[8] = {0, 0, 0, 0, 0, 0, 0, 0};
         double t_enqueue = 0, t_wait = 0;  // (RT_AMD_SERIAL_DEBUG)
         hipEvent_t dbg_ev[2] = {nullptr, nullptr};
+        unsigned long long *dbg_cnt = nullptr;  // (coalescing search counters)
         if (env_u64("RT_AMD_SERIAL_DEBUG", 0)) {
             for (auto &e : dbg_ev) HIP_TRY(hipEventCreate(&e));
             HIP_TRY(hipEventRecord(dbg_ev[0], s));
+            HIP_TRY(hipMalloc((void **)&dbg_cnt, 4 * 8));
+            HIP_TRY(hipMemsetAsync(dbg_cnt, 0, 4 * 8, s));
         }
         const double t_prep = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tp0).count();
         uint64_t queued = 0;
@@ -952,15 +986,19 @@ static int serial_find_states(WorldState &w, const CameraModel &cam, size_t widt
             for (uint64_t q = 0; q < it; ++q) {
                 HIP_TRY(launch_serial_window(d->sctrl, d->sjump, d->swin, (uint32_t)wlen, pred, d->slo,
                                              (uint32_t)L, (uint32_t)K, depth, (uint32_t)N, s));
-                const SerialPass sp{kRngSerialCount, 0u, (uint32_t)L, (uint32_t)K, d->swin, pred,
-                                    d->sctrl, d->slo};
+                SerialPass sp{coalesce ? kRngSerialCoalesce : kRngSerialCount, 0u, (uint32_t)L, (uint32_t)K,
+                              d->swin, pred, d->sctrl, d->slo};
+                sp.path = d->spath;
+                sp.bend = d->sbend;
+                sp.R = (uint32_t)R_walk;
+                sp.dbg = dbg_cnt;
                 rc = render_frame(w, cam, width, height, ob, nullptr, s, nullptr, &sp);
                 if (rc) return rc;
-                HIP_TRY(launch_serial_walk(d->sctrl, d->samples, pred, adapt ? Vdev : nullptr,
+                HIP_TRY(launch_serial_walk(d->sctrl, coalesce ? nullptr : d->samples, pred, adapt ? Vdev : nullptr,
                                            (uint32_t)npix, (uint32_t)spp, (float)z, (float)serial_floor(spp * R),
                                            d->swin, d->sstates, d->sbend, gather ? d->spath : nullptr,
                                            gather ? d->sfin : nullptr, d->slo, d->ssbend, d->ssb, (uint32_t)L,
-                                           (uint32_t)Lw, (uint32_t)K, depth,
+                                           (uint32_t)Lw, (uint32_t)K, (uint32_t)R_walk, depth,
                                            (uint32_t)N, s));
             }
             const auto t1 = std::chrono::steady_clock::now();
@@ -983,11 +1021,19 @@ static int serial_find_states(WorldState &w, const CameraModel &cam, size_t widt
             HIP_TRY(hipEventElapsedTime(&b, dbg_ev[0], dbg_ev[1]));
             std::fprintf(stderr, "serial debug: GPU estimate + tables %.1f ms, iterations %.1f ms\n", a, b);
             for (auto &e : dbg_ev) (void)hipEventDestroy(e);
+            unsigned long long c[4] = {0, 0, 0, 0};
+            HIP_TRY(hipMemcpy(c, dbg_cnt, sizeof(c), hipMemcpyDeviceToHost));
+            HIP_TRY(hipFree(dbg_cnt));
+            if (coalesce && c[2])
+                std::fprintf(stderr, "serial debug: coalesce %llu traces in %llu blocks (%.3f of the count pass's "
+                             "%llu), %.1f trace passes per block\n", c[0], c[2], (double)c[0] / std::max(1.0, (double)c[3]),
+                             c[3], (double)c[1] / (double)c[2]);
         }
         if (env_u64("RT_AMD_SERIAL_DEBUG", 0)) {
-            std::fprintf(stderr, "serial debug: N %llu L %llu K %llu sigma %.3f: %u iterations (%u "
+            std::fprintf(stderr, "serial debug: %s N %llu L %llu R %llu K %llu sigma %.3f: %u iterations (%u "
                          "stopped short), %llu queued, estimate + tables %.1f ms, enqueue %.1f ms, wait %.1f ms\n",
-                         (unsigned long long)N, (unsigned long long)L, (unsigned long long)K, sigma,
+                         coalesce ? "coalesce" : "count", (unsigned long long)N, (unsigned long long)L,
+                         (unsigned long long)R_walk, (unsigned long long)K, sigma,
                          ctrl[3], ctrl[6], (unsigned long long)queued, t_prep, t_enqueue, t_wait);
         }
     }

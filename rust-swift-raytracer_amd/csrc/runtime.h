@@ -78,7 +78,7 @@ struct DeviceState {
     uint32_t *swin = nullptr;        size_t swin_cap = 0;
     uint32_t *sbend = nullptr;       size_t sbend_cap = 0;
     uint32_t *spath = nullptr;       size_t spath_cap = 0;  // block walks' paths (L x K)
-    uint32_t *sfin = nullptr;                               // chain result (4 + 256)
+    uint32_t *sfin = nullptr;                               // chain result (4 + kMaxWalkBlocks)
     uint32_t *sjump = nullptr;
     uint32_t *sctrl = nullptr;
     unsigned long long *scheck = nullptr;                       // chain-check count
@@ -133,6 +133,11 @@ struct SerialPass {
     SerialPred M;
     const uint32_t *ctrl;
     const uint32_t *lo;       // kRngSerialCount (optional): tabulated window bases
+    // kRngSerialCoalesce: the block walks' outputs (launch_serial_coalesce),
+    // iteration length (nsamples), candidates (variants) and block length R
+    uint32_t *path = nullptr, *bend = nullptr;
+    uint32_t R = 0;
+    unsigned long long *dbg = nullptr;  // (RT_AMD_SERIAL_DEBUG: launch_serial_coalesce's counters)
 };
 
 // Renders rank's tile of a width x height frame into device memory d_out

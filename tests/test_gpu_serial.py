@@ -2,10 +2,11 @@
 stream (common.rs:321, random.rs:8-30) found on the device -- no replay table
 from a CPU run -- against the oracle's SERIAL mode, bit for bit.
 
-The library traces the next samples from candidate stream positions, walks
-the true path through that table as far as it stays inside the candidate
-windows, repeats from there, and renders from the start states it found
-(runtime.cpp render_frame_serial).  Cases: the
+The library traces the next samples from candidate stream positions (every
+candidate: the count pass; or each block's distinct live offsets: the
+coalescing search), follows the true path as far as it stays inside the
+candidate windows, repeats from there, and renders from the start states it
+found (runtime.cpp render_frame_serial).  Cases: the
 examples/c_raytracer.rs frame (200x200, 16 spp, depth 8 -- render()'s
 settings, lib.rs:51), BASELINE configs[0] (C1), the sphere BVH (RTOW) and the
 triangle trees, edge frames, row tiles, a non-default seed, and windows forced
@@ -77,10 +78,11 @@ def test_serial_narrow_windows_and_short_iterations(monkeypatch):
         (dict(RT_AMD_SERIAL_K="24", RT_AMD_SERIAL_CHUNK="512"), "c_raytracer_world.txt", (80, 60, 16, 8)),
         (dict(RT_AMD_SERIAL_ADAPT="0"), "c_raytracer_world.txt", (40, 30, 16, 8)),
         (dict(RT_AMD_SERIAL_ADAPT="0", RT_AMD_SERIAL_CHUNK="700"), "world.txt", (33, 17, 3, 8)),
-        # resolved states re-walked per block instead of gathered from the block paths
-        (dict(RT_AMD_SERIAL_GATHER="0"), "c_raytracer_world.txt", (40, 30, 16, 8)),
-        (dict(RT_AMD_SERIAL_GATHER="0", RT_AMD_SERIAL_K="24", RT_AMD_SERIAL_CHUNK="300"), "world.txt",
-         (29, 13, 4, 8)),
+        # resolved states re-walked per block instead of gathered from the block
+        # paths (the count pass: the coalescing search always gathers)
+        (dict(RT_AMD_SERIAL_GATHER="0", RT_AMD_SERIAL_COALESCE="0"), "c_raytracer_world.txt", (40, 30, 16, 8)),
+        (dict(RT_AMD_SERIAL_GATHER="0", RT_AMD_SERIAL_COALESCE="0", RT_AMD_SERIAL_K="24",
+              RT_AMD_SERIAL_CHUNK="300"), "world.txt", (29, 13, 4, 8)),
         (dict(RT_AMD_SERIAL_CHUNK="1"), "world.txt", (12, 9, 2, 8)),
         (dict(RT_AMD_SERIAL_CHUNK="100"), "world.txt", (13, 7, 3, 8)),
         (dict(RT_AMD_SERIAL_CHUNK="100000", RT_AMD_SERIAL_Z10="5"), "world.txt", (31, 17, 4, 8)),
@@ -88,12 +90,40 @@ def test_serial_narrow_windows_and_short_iterations(monkeypatch):
         (dict(RT_AMD_SERIAL_CHUNK="37"), "world.txt", (15, 9, 3, 1)),
         (dict(RT_AMD_SERIAL_CHUNK="61", RT_AMD_SERIAL_K="4"), "world.txt", (15, 9, 3, 1)),
         # count-pass scheduling: small chunks of any size, many partitions
-        (dict(RT_AMD_SERIAL_CCHUNK="37", RT_AMD_SERIAL_PARTS="256"), "c_raytracer_world.txt", (40, 30, 16, 8)),
+        (dict(RT_AMD_SERIAL_COALESCE="0", RT_AMD_SERIAL_CCHUNK="37", RT_AMD_SERIAL_PARTS="256"),
+         "c_raytracer_world.txt", (40, 30, 16, 8)),
+        # coalescing search: blocks of 1 and 7 samples, narrow windows in long blocks
+        (dict(RT_AMD_SERIAL_R="1", RT_AMD_SERIAL_CHUNK="300"), "c_raytracer_world.txt", (20, 15, 4, 8)),
+        (dict(RT_AMD_SERIAL_R="7", RT_AMD_SERIAL_CHUNK="1000"), "world.txt", (33, 17, 3, 8)),
+        (dict(RT_AMD_SERIAL_R="200", RT_AMD_SERIAL_K="24", RT_AMD_SERIAL_CHUNK="4000"), "world.txt",
+         (40, 30, 4, 8)),
     ]:
         for k, v in env.items():
             monkeypatch.setenv(k, v)
         img, st, out, gst, _ = _serial_pair(scene_text(scene), *size)
         assert_bits_equal(out, img, f"SERIAL frame {env}")
+        assert gst["rays"] == st["rays"]
+        for k in env:
+            monkeypatch.delenv(k)
+
+
+@pytest.mark.parametrize("coalesce", ["0", "1"])
+def test_serial_search_modes(monkeypatch, coalesce):
+    """Both start-state searches on every scene family: the count pass + block
+    walks and the coalescing block search (runtime.cpp picks coalescing for
+    brute-force scenes, the count pass where trees exist), on small scenes,
+    the sphere tree and triangle trees, with wide and narrow windows."""
+    monkeypatch.setenv("RT_AMD_SERIAL_COALESCE", coalesce)
+    for src, size, env in [
+        (scene_text("c_raytracer_world.txt"), (64, 48, 8, 8), {}),
+        (scene_text("world.txt"), (48, 27, 16, 8), dict(RT_AMD_SERIAL_K="30", RT_AMD_SERIAL_CHUNK="2000")),
+        (S.rtow(), (48, 27, 4, 8), {}),
+        (S.triangle_soup(11, 200, spheres=20, grid=5), (40, 30, 4, 8), dict(RT_AMD_SERIAL_CHUNK="1500")),
+    ]:
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
+        img, st, out, gst, _ = _serial_pair(src, *size)
+        assert_bits_equal(out, img, f"SERIAL frame, coalesce={coalesce} {env}")
         assert gst["rays"] == st["rays"]
         for k in env:
             monkeypatch.delenv(k)
