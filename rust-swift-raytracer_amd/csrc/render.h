@@ -210,6 +210,8 @@ hipError_t launch_serial_window(const uint32_t *ctrl, const uint32_t *jump, uint
 hipError_t launch_serial_coalesce(const TraceParams &p, uint32_t *path, uint32_t *bend, uint32_t L, uint32_t Kmax,
                                   uint32_t R, bool tree_lds, unsigned long long *dbg, hipStream_t stream);
 size_t serial_coalesce_lds(const TraceParams &p, uint32_t K, bool tree_lds);
+// the search's own LDS bytes (without the tree) for K candidates at this depth
+size_t serial_coalesce_search_lds(uint32_t K, uint32_t depth);
 // Walk: from sample a = ctrl[4], follows the true path through the candidate
 // table (b of chunk sample jl at candidate k = table[jl * K + k], plane 0 of
 // the slab) as far as it stays inside the candidate windows (at least one

@@ -2035,6 +2035,8 @@ static void launch_coalesce_m(const TraceParams &p, uint32_t *path, uint32_t *be
                            path, bend, L, Kmax, R, (uint32_t)tree_bytes, dbg);
 }
 
+size_t serial_coalesce_search_lds(uint32_t K, uint32_t depth) { return coalesce_lds_bytes(K, depth); }
+
 size_t serial_coalesce_lds(const TraceParams &p, uint32_t K, bool tree_lds) {
     const size_t tb = tree_lds ? (trace_lds_bytes(p) + 15) & ~(size_t)15 : 0;
     return tb + coalesce_lds_bytes(K, p.depth > 0 ? (uint32_t)p.depth : 0u);

@@ -914,8 +914,8 @@ static int serial_find_states(WorldState &w, const CameraModel &cam, size_t widt
             return -5;
         }
         // (the coalescing workgroup keeps K candidates' u16 slots and K + depth
-        // + 1 live offsets in LDS: wider windows take the count pass)
-        if (K > 4096) coalesce = false;
+        // + 1 live offsets in LDS, <= 64 KB: wider windows take the count pass)
+        if (K > 4096 || serial_coalesce_search_lds((uint32_t)K, depth) > 64 * 1024) coalesce = false;
         // The walks size each iteration's windows from the per-pixel variances
         // (V: prefix sums over pixels of spp var, then var; the variance of
         // samples [0, j) is PV[p] + (j - p spp) var[p]): 2 z (sqrt(V) + 0.05
