@@ -141,8 +141,6 @@ struct TraceParams {
     uint32_t sspp;            // the frame's spp ...
     FastDiv div_sspp;         // ... and its divider
     uint32_t max_draws;       // 2 + 3 * max(depth, 0): bound of the draw count search
-    const uint8_t *ssky;      // SERIAL searches (optional): 1 for pixels no primary ray can
-                              // hit anything from (launch_serial_sky): b = 0, no trace
 };
 
 // Candidate k of chunk sample jl (frame sample a + jl) means B = serial_lo + k
@@ -214,13 +212,6 @@ hipError_t launch_serial_coalesce(const TraceParams &p, uint32_t *path, uint32_t
 size_t serial_coalesce_lds(const TraceParams &p, uint32_t K, bool tree_lds);
 // the search's own LDS bytes (without the tree) for K candidates at this depth
 size_t serial_coalesce_search_lds(uint32_t K, uint32_t depth);
-// sky[p] = 1 for every pixel p (frame order, row = p / width as ray_trace
-// counts rows) whose every primary ray provably hits no sphere (nsph of
-// sph_hot) and no triangle phantom (ntri of tri_geo); cam: as TraceParams::cam
-struct SkyCamera { float c[12]; };
-hipError_t launch_serial_sky(const float4 *sph_hot, uint32_t nsph, const float4 *tri_geo, uint32_t ntri,
-                             const SkyCamera &cam, uint32_t width, uint32_t height, uint8_t *sky,
-                             hipStream_t stream);
 // Walk: from sample a = ctrl[4], follows the true path through the candidate
 // table (b of chunk sample jl at candidate k = table[jl * K + k], plane 0 of
 // the slab) as far as it stays inside the candidate windows (at least one

@@ -1870,105 +1870,6 @@ __device__ __forceinline__ uint32_t serial_trace_b(const TraceParams &p, const B
     return b;  // depth exhausted (common.rs:284)
 }
 
-// ---- pixels whose every primary ray misses everything (SERIAL searches)
-// A sample that hits nothing draws only u and v (common.rs:276-281, 335-336):
-// b = 0 from any stream state, so the searches skip its traces.  Per pixel, a
-// conservative test in double: the cone around the pixel's four corner rays
-// (u in [col, col + 1] / (W - 1), v likewise, camera.rs:84-89) against a ball
-// around every primitive -- a sphere, or the bounding ball of a triangle's
-// phantom (the triangle moved by 2 (n^.o) n^: the reference's t = (n.o + d) /
-// cos puts the hit on that plane, common.rs:141, and the edge tests only see
-// its projection) -- with relative margins far above float rounding (1e-3 of
-// the radius, 1e-4 of the distance, 1e-4 rad).  Any non-finite input, or a
-// camera inside or touching a ball, flags no pixel of that ball's cone.
-__global__ __launch_bounds__(256) void serial_sky_kernel(const float4 *__restrict__ sph_hot, uint32_t nsph,
-                                                         const float4 *__restrict__ tri_geo, uint32_t ntri,
-                                                         SkyCamera camera, uint32_t width, uint32_t height,
-                                                         uint8_t *__restrict__ sky) {
-    const float *cam = camera.c;
-    const uint32_t pix = blockIdx.x * blockDim.x + threadIdx.x;
-    if (pix >= width * height) return;
-    const uint32_t row = pix / width, col = pix - row * width;  // (row as ray_trace counts it)
-    const double o[3] = {cam[0], cam[1], cam[2]};
-    const double wd = (double)(width - 1), hd = (double)(height - 1);
-    double ax[3] = {0.0, 0.0, 0.0}, e[4][3];
-    bool ok = wd > 0.0 && hd > 0.0;
-    for (int k = 0; k < 4 && ok; ++k) {
-        const double u = ((double)col + (k & 1 ? 1.0 : 0.0)) / wd, v = ((double)row + (k & 2 ? 1.0 : 0.0)) / hd;
-        double n2 = 0.0;
-        for (int c = 0; c < 3; ++c) {
-            e[k][c] = (((double)cam[3 + c] + (double)cam[6 + c] * u) + (double)cam[9 + c] * v) - o[c];
-            n2 += e[k][c] * e[k][c];
-        }
-        const double n = sqrt(n2);
-        ok = n > 0.0 && isfinite(n);
-        for (int c = 0; c < 3; ++c) { e[k][c] /= n; ax[c] += e[k][c]; }
-    }
-    const double an = sqrt(ax[0] * ax[0] + ax[1] * ax[1] + ax[2] * ax[2]);
-    ok = ok && an > 0.0 && isfinite(an);
-    double cos_cone = 1.0;
-    for (int k = 0; k < 4 && ok; ++k) {
-        double d = 0.0;
-        for (int c = 0; c < 3; ++c) d += e[k][c] * ax[c] / an;
-        cos_cone = fmin(cos_cone, d);
-    }
-    const double cone = ok ? acos(fmax(-1.0, fmin(1.0, cos_cone))) + 1e-4 : 0.0;
-    // a ball (centre c, radius r) the pixel's rays may reach
-    auto reaches = [&](const double c[3], double r) {
-        double w[3], dist2 = 0.0, dot = 0.0;
-        for (int k = 0; k < 3; ++k) { w[k] = c[k] - o[k]; dist2 += w[k] * w[k]; dot += w[k] * ax[k] / an; }
-        const double dist = sqrt(dist2);
-        const double rr = fabs(r) * 1.001 + 1e-4 * dist + 1e-6;
-        if (!(isfinite(dist) && isfinite(rr)) || dist <= rr) return true;
-        const double phi = acos(fmax(-1.0, fmin(1.0, dot / dist)));
-        return phi <= cone + asin(rr / dist) + 1e-4;
-    };
-    bool hit = !ok;
-    for (uint32_t i = 0; i < nsph && !hit; ++i) {
-        const float4 S = sph_hot[i];
-        const double c[3] = {S.x, S.y, S.z};
-        hit = reaches(c, sqrt(fabs((double)S.w)));
-    }
-    for (uint32_t i = 0; i < ntri && !hit; ++i) {
-        const float4 *g = tri_geo + 4u * i;
-        const float4 A = g[0], B = g[1], C = g[2], N = g[3];
-        const double nn = sqrt((double)N.x * N.x + (double)N.y * N.y + (double)N.z * N.z);
-        double sh[3] = {0.0, 0.0, 0.0};
-        if (nn > 0.0 && isfinite(nn)) {
-            const double s2 = 2.0 * (((double)N.x * o[0] + (double)N.y * o[1]) + (double)N.z * o[2]) / (nn * nn);
-            sh[0] = s2 * N.x; sh[1] = s2 * N.y; sh[2] = s2 * N.z;
-        } else {
-            hit = true;  // (no usable normal: assume it may be hit)
-            break;
-        }
-        const double v[3][3] = {{A.x + sh[0], A.y + sh[1], A.z + sh[2]},
-                                {B.x + sh[0], B.y + sh[1], B.z + sh[2]},
-                                {C.x + sh[0], C.y + sh[1], C.z + sh[2]}};
-        double c[3];
-        for (int k = 0; k < 3; ++k) c[k] = (v[0][k] + v[1][k] + v[2][k]) / 3.0;
-        double r = 0.0;
-        for (int q = 0; q < 3; ++q) {
-            double d2 = 0.0;
-            for (int k = 0; k < 3; ++k) d2 += (v[q][k] - c[k]) * (v[q][k] - c[k]);
-            r = fmax(r, sqrt(d2));
-        }
-        // (plus the rounding of the phantom shift: 1e-4 of |o| and the vertices)
-        const double mag = fabs(o[0]) + fabs(o[1]) + fabs(o[2]) + fabs(c[0]) + fabs(c[1]) + fabs(c[2]);
-        hit = reaches(c, r + 1e-4 * mag);
-    }
-    sky[pix] = hit ? 0 : 1;
-}
-
-hipError_t launch_serial_sky(const float4 *sph_hot, uint32_t nsph, const float4 *tri_geo, uint32_t ntri,
-                             const SkyCamera &cam, uint32_t width, uint32_t height, uint8_t *sky,
-                             hipStream_t stream) {
-    const uint64_t n = (uint64_t)width * height;
-    if (!n) return hipSuccess;
-    hipLaunchKernelGGL(serial_sky_kernel, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, stream, sph_hot, nsph,
-                       tri_geo, ntri, cam, width, height, sky);
-    return hipGetLastError();
-}
-
 // Exclusive prefix sum of one u32 per thread over the 256-thread workgroup
 // (wave scans, then the 4 wave totals); *total gets the sum.  Contains barriers.
 __device__ __forceinline__ uint32_t block_exscan256(uint32_t v, uint32_t *wsum, uint32_t *total) {
@@ -2054,15 +1955,12 @@ __global__ __launch_bounds__(kCoalesceThreads) void serial_coalesce_kernel(Trace
         const uint32_t l = p.slo[jl];  // the window of sample jl: [l, l + K)
         uint32_t *bits = (s & 1u) ? bits1 : bits0;
         uint32_t *bnext = (s & 1u) ? bits0 : bits1;
-        // every distinct live offset once: its sample's end offset (a sample
-        // of a sky pixel scatters 0 times from any state: no trace)
-        const bool sky = p.ssky != nullptr && p.ssky[fdiv(a + jl, p.div_sspp)] != 0;
+        // every distinct live offset once: its sample's end offset
         for (uint32_t i = t; i < nlive; i += kCoalesceThreads) {
             const uint32_t B = LB[i];
             uint32_t e = kSlotDead;
             if (B >= l && B - l < K) {
-                e = sky ? B
-                        : B + serial_trace_b<kBvh, kLds, kMesh>(p, view, sph_root, p.win[2u * jl + 3u * B], a + jl);
+                e = B + serial_trace_b<kBvh, kLds, kMesh>(p, view, sph_root, p.win[2u * jl + 3u * B], a + jl);
                 const uint32_t r = e - l;  // < K + depth
                 atomicOr(&bits[r >> 5], 1u << (r & 31u));
             }

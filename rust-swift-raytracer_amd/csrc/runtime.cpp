@@ -53,7 +53,7 @@ DeviceState::~DeviceState() {
                     bvh_nodes, bvh_prims, big_hot, bvh_miss, bvh_prim_id, big_id, bvh_miss16,
                     sph_shade, sph_kind, tbvh_nodes, tbvh_tris, tbvh_loose,
                     cam_nodes, cam_tris, ptl_off, ptl_items, spl, tile, gath,
-                    sstates, stab, sscan, swin, sjump, sctrl, sbend, spath, sfin, ssky,
+                    sstates, stab, sscan, swin, sjump, sctrl, sbend, spath, sfin,
                     gspl, gspl_rects, gspl_flag, scheck, slo, ssbend, ssb};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
@@ -595,7 +595,6 @@ int render_frame(WorldState &w, const CameraModel &cam, size_t width, size_t hei
         p.sM = sp->M;
         p.slo = sp->lo;
         p.ctrl = sp->ctrl;
-        p.ssky = sp->sky;
         p.max_draws = 2u + 3u * (uint32_t)std::max(o.max_ray_bounces, 0);
         p.njobs = (uint32_t)njobs;
         p.npix = sp->nsamples;
@@ -960,19 +959,6 @@ static int serial_find_states(WorldState &w, const CameraModel &cam, size_t widt
             HIP_TRY(hipMemcpy(d->sjump, jt.data(), jt.size() * 4, hipMemcpyHostToDevice));
         }
         if (!d->sctrl) HIP_TRY(hipMalloc((void **)&d->sctrl, 32));
-        // pixels whose every primary ray provably misses everything: b = 0 from
-        // any state, no trace (the coalescing search; scenes of <= 4096
-        // primitives: one thread per pixel tests them all)
-        const uint8_t *sky = nullptr;
-        if (coalesce && env_u64("RT_AMD_SERIAL_SKY", 1) != 0 && (uint64_t)d->nsph + d->ntri <= 4096) {
-            HIP_TRY(grow(d->ssky, d->ssky_cap, npix));
-            SkyCamera sc{};
-            const Vec3 cv[4] = {cam.origin, cam.lower_left, cam.horizontal, cam.vertical};
-            for (int i = 0; i < 4; ++i) { sc.c[3 * i] = cv[i].x; sc.c[3 * i + 1] = cv[i].y; sc.c[3 * i + 2] = cv[i].z; }
-            HIP_TRY(launch_serial_sky(d->sph_hot, d->nsph, d->tri_geo, d->ntri, sc, (uint32_t)width,
-                                      (uint32_t)height, d->ssky, s));
-            sky = d->ssky;
-        }
         const uint32_t ctrl0[8] = {0u, o.seed, 0u, 0u, 0u, K0, 0u, 0u};  // Random::new() (random.rs:8-10)
         HIP_TRY(hipMemcpyAsync(d->sctrl, ctrl0, 32, hipMemcpyHostToDevice, s));
         // iterations are queued in batches sized by the expected progress;
@@ -1006,7 +992,6 @@ static int serial_find_states(WorldState &w, const CameraModel &cam, size_t widt
                 sp.bend = d->sbend;
                 sp.R = (uint32_t)R_walk;
                 sp.dbg = dbg_cnt;
-                sp.sky = sky;
                 rc = render_frame(w, cam, width, height, ob, nullptr, s, nullptr, &sp);
                 if (rc) return rc;
                 HIP_TRY(launch_serial_walk(d->sctrl, coalesce ? nullptr : d->samples, pred, adapt ? Vdev : nullptr,

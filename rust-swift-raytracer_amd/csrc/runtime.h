@@ -70,7 +70,6 @@ struct DeviceState {
     // SERIAL mode (render_frame_serial): start states, candidate offsets, the
     // stream window of a chunk, xorshift jump matrices, control block
     uint32_t *sstates = nullptr;     size_t sstates_cap = 0;
-    uint8_t *ssky = nullptr;         size_t ssky_cap = 0;   // SERIAL: pixels no primary ray can hit from
     double *stab = nullptr;          size_t stab_cap = 0;   // prediction tables (render.h serial_tab_doubles)
     double *sscan = nullptr;         size_t sscan_cap = 0;  // their scan's scratch
     uint32_t *slo = nullptr;         size_t slo_cap = 0;    // an iteration's window bases (launch_serial_window)
@@ -139,7 +138,6 @@ struct SerialPass {
     uint32_t *path = nullptr, *bend = nullptr;
     uint32_t R = 0;
     unsigned long long *dbg = nullptr;  // (RT_AMD_SERIAL_DEBUG: launch_serial_coalesce's counters)
-    const uint8_t *sky = nullptr;       // launch_serial_sky's flags (TraceParams::ssky)
 };
 
 // Renders rank's tile of a width x height frame into device memory d_out
