@@ -1900,8 +1900,16 @@ __host__ __device__ inline size_t coalesce_lds_bytes(uint32_t K, uint32_t depth)
     return al(2 * (size_t)K) + 3 * al(4 * Kp) + 3 * al(4 * W) + 16;
 }
 
+// Waves per SIMD the brute-force coalescing kernels are compiled for (their
+// live set fits 64 VGPRs without spills at 8; 1 = unconstrained, 76 VGPRs, 6
+// waves); the tree variants stay unconstrained (they would spill at 8)
+#ifndef RT_COALESCE_WAVES_BRUTE
+#define RT_COALESCE_WAVES_BRUTE 8
+#endif
 template <bool kBvh, bool kLds, int kMesh>
-__global__ __launch_bounds__(kCoalesceThreads) void serial_coalesce_kernel(TraceParams p, uint32_t *__restrict__ path,
+__global__ __launch_bounds__(kCoalesceThreads)
+__attribute__((amdgpu_waves_per_eu(kBvh ? 1 : RT_COALESCE_WAVES_BRUTE, 8)))
+void serial_coalesce_kernel(TraceParams p, uint32_t *__restrict__ path,
                                                                            uint32_t *__restrict__ bend, uint32_t L,
                                                                            uint32_t Kmax, uint32_t R,
                                                                            uint32_t tree_bytes,
