@@ -171,6 +171,15 @@ static int device_for(WorldState &w, int want, DeviceState *&out) {
                         fits = fits && d->blocks_per_cu_lds[c][st] > 0;
                     }
                 if (fits) d->lds_bytes = lds;
+                if (fits && !tri) {
+                    const size_t plds = pixel_lds_bytes(lp);
+                    bool pfits = true;
+                    for (int c = 0; c < 2; ++c) {
+                        HIP_TRY(pixel_occupancy(&d->blocks_per_cu_pix[c], plds, c));
+                        pfits = pfits && d->blocks_per_cu_pix[c] > 0;
+                    }
+                    if (pfits) d->pix_lds = plds;
+                }
             }
         }
         const TriangleBVH &tb = w.tbvh;
@@ -559,7 +568,12 @@ int render_frame(WorldState &w, const CameraModel &cam, size_t width, size_t hei
     const int sv = p.step ? 1 : 0;
     const bool timed = stats != nullptr;  // HIP-event timing + counters need a host wait
     const int ctv = timed ? 1 : 0;         // launch_trace runs the counting variant iff p.stats
-    const int bpc = !use_bvh   ? d->blocks_per_cu[ctv][sv]
+    // one pixel per lane (pixel_kernel): sphere-only frames with
+    // the tree in LDS and the fused resolve; RT_AMD_PIXEL=0 keeps trace_kernel
+    const bool pixmode = fused && !sp && use_bvh && p.use_lds && d->ntri == 0 && d->pix_lds > 0 &&
+                         env_u64("RT_AMD_PIXEL", 1) != 0;
+    const int bpc = pixmode    ? d->blocks_per_cu_pix[ctv]
+                    : !use_bvh  ? d->blocks_per_cu[ctv][sv]
                     : p.use_lds ? d->blocks_per_cu_lds[ctv][sv]
                                 : d->blocks_per_cu_bvh[ctv][sv];
     const uint64_t waves_per_block = trace_block_threads(use_bvh && p.use_lds, p.ntri != 0) / 64;
@@ -636,7 +650,35 @@ int render_frame(WorldState &w, const CameraModel &cam, size_t width, size_t hei
         p.njobs = (uint32_t)njobs;
         p.npix = (uint32_t)(rows * width);
         if (timed) HIP_TRY(hipEventRecord(d->ev[0], s));
-        if (njobs) {
+        if (njobs && pixmode) {
+            // pixels per lane: >= 16 samples per lane before the grid shrinks
+            const uint64_t per_block = waves_per_block * 64;
+            uint64_t blocks = std::min<uint64_t>(full_blocks, (njobs + 16 * per_block - 1) / (16 * per_block));
+            blocks = std::max<uint64_t>(blocks, 1);
+            const uint64_t nwaves = blocks * waves_per_block;
+            const uint64_t npix = rows * width;
+            // a wave's first pull fills its lanes (or shares the launch's
+            // pixels out evenly); later pulls take up to 64
+            p.chunk0 = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(64, npix / nwaves));
+            uint64_t chunk = env_u64("RT_AMD_PIX_CHUNK", 0);
+            if (!chunk) chunk = std::max<uint64_t>(1, std::min<uint64_t>(64, npix / (2 * nwaves)));
+            p.chunk = (uint32_t)chunk;
+            uint64_t parts = env_u64("RT_AMD_PARTS", 16);
+            parts = std::max<uint64_t>(1, std::min<uint64_t>({parts, kMaxParts, npix / (16 * chunk) + 1}));
+            p.nparts = (uint32_t)parts;
+            HIP_TRY(grow(d->ring, d->ring_cap, nwaves * pixel_help_floats()));
+            HIP_TRY(grow(d->psum, d->psum_cap, npix));
+            p.ring = d->ring;
+            p.ring_shift = 0;
+            p.psum = d->psum;
+            HIP_TRY(hipMemsetAsync(d->counter, 0, parts * 128, s));
+            HIP_TRY(launch_pixel(p, (uint32_t)blocks, s));
+            d->last_jobs = 0;
+            d->last_spp = spp;
+            d->last_fused = true;
+            ++launches;
+            waves = (uint32_t)nwaves;
+        } else if (njobs) {
             const uint64_t jobs_per_block = waves_per_block * 256;
             uint64_t blocks = std::min<uint64_t>(full_blocks, (njobs + jobs_per_block - 1) / jobs_per_block);
             blocks = std::max<uint64_t>(blocks, 1);
@@ -688,7 +730,8 @@ int render_frame(WorldState &w, const CameraModel &cam, size_t width, size_t hei
             waves = (uint32_t)nwaves;
         }
         if (timed) HIP_TRY(hipEventRecord(d->ev[1], s));
-        if (!fused)  // (spp 0: no samples, the resolve still writes every pixel)
+        if (!fused)  // (spp 0: no samples, the resolve still writes every pixel; the
+                     // pixel kernel's epilogue is part of launch_pixel)
             HIP_TRY(launch_resolve_ex(d->samples, d_out, (uint32_t)(rows * width), spp, inv_spp,
                                       (uint32_t)width, (uint32_t)r0, s));
         if (timed) {
@@ -821,6 +864,10 @@ static int serial_find_states(WorldState &w, const CameraModel &cam, size_t widt
     HIP_TRY(hipEventRecord(d->sev[0], s));
     HIP_TRY(grow(d->sstates, d->sstates_cap, std::max<uint64_t>(N, 1)));
     RtRenderOptions ob = o;
+    // the inner passes read and write d's buffers (d->samples, d->stab, ...):
+    // pin them to d's device rather than to whichever device is current
+    ob.device = d->device;
+    ob.ndevices = 0;
     ob.rng_mode = RT_RNG_COUNTER;
     ob.rank = 0;
     ob.nranks = 1;
@@ -848,8 +895,11 @@ static int serial_find_states(WorldState &w, const CameraModel &cam, size_t widt
         // scenes, i.e. no sphere or triangle tree (< 16 of each: render()'s
         // scenes; 960x540x16 c_raytracer 338 -> 308 ms, world.txt 301 -> 233
         // ms) -- and loses on tree walks (RTOW 238 -> 620 ms).
-        // RT_AMD_SERIAL_COALESCE: 0 off, 1 on, unset: that rule.
-        const bool trees = o.accel != RT_ACCEL_BRUTE && (d->nnodes > 0 || d->tnodes > 0);
+        // RT_AMD_SERIAL_COALESCE: 0 off, 1 on, unset: that rule.  The rule
+        // keys on the scene's size (trees are built for >= 16 spheres or
+        // triangles), not on o.accel: a large scene forced to RT_ACCEL_BRUTE
+        // has even longer traces and takes the count pass too.
+        const bool trees = d->nnodes > 0 || d->tnodes > 0;
         bool coalesce = env_u64("RT_AMD_SERIAL_COALESCE", trees ? 0 : 1) != 0 && depth < 1024;
         // (iterations of 128 k samples in blocks of 32 for the coalescing search,
         // profiles/round3_serial/coalesce_sweep*.log; 16 k for the count pass)
@@ -1042,27 +1092,38 @@ static int serial_find_states(WorldState &w, const CameraModel &cam, size_t widt
         // the chain the reference's one stream forms (common.rs:321-341):
         // sample 0 starts at the seed, sample j ends where j + 1 starts,
         // the last one where the search ended (ctrl[1])
+        // the states the check traces: d->sstates, or (test hook) a scratch
+        // copy with one state corrupted, so the check must see the links into
+        // and out of that sample break while the frame still renders from the
+        // states the search found
+        const uint32_t *checked = d->sstates;
+        uint32_t *broken = nullptr;
         if (const char *brk = std::getenv("RT_AMD_SERIAL_BREAK")) {
-            // (tests: corrupt one found start state, so the check must see the
-            // links into and out of that sample break)
             const uint64_t j = std::strtoull(brk, nullptr, 10);
             if (j < N) {
+                HIP_TRY(hipMalloc((void **)&broken, N * 4));
+                HIP_TRY(hipMemcpyAsync(broken, d->sstates, N * 4, hipMemcpyDeviceToDevice, s));
                 uint32_t x = 0;
-                HIP_TRY(hipMemcpyAsync(&x, d->sstates + j, 4, hipMemcpyDeviceToHost, s));
+                HIP_TRY(hipMemcpyAsync(&x, broken + j, 4, hipMemcpyDeviceToHost, s));
                 HIP_TRY(hipStreamSynchronize(s));
                 x = x == 1u ? 2u : 1u;
-                HIP_TRY(hipMemcpyAsync(d->sstates + j, &x, 4, hipMemcpyHostToDevice, s));
+                HIP_TRY(hipMemcpyAsync(broken + j, &x, 4, hipMemcpyHostToDevice, s));
                 HIP_TRY(hipStreamSynchronize(s));
+                checked = broken;
             }
         }
+        struct FreeScratch {
+            uint32_t *p;
+            ~FreeScratch() { if (p) (void)hipFree(p); }
+        } free_broken{broken};
         uint32_t first = 0;
-        HIP_TRY(hipMemcpyAsync(&first, d->sstates, 4, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipMemcpyAsync(&first, checked, 4, hipMemcpyDeviceToHost, s));
         if (!d->scheck) HIP_TRY(hipMalloc((void **)&d->scheck, 8));
         HIP_TRY(hipMemsetAsync(d->scheck, 0, 8, s));
         const uint64_t step = 1ull << 28;
         for (uint64_t c0 = 0; c0 < N; c0 += step) {
             const uint32_t n = (uint32_t)std::min(step, N - c0);
-            const SerialPass sp{kRngSerialCheck, (uint32_t)c0, n, 1u, d->sstates, SerialPred{}, nullptr};
+            const SerialPass sp{kRngSerialCheck, (uint32_t)c0, n, 1u, checked, SerialPred{}, nullptr};
             RtRenderOptions oc = ob;
             oc.seed = final_state;
             rc = render_frame(w, cam, width, height, oc, nullptr, s, nullptr, &sp);

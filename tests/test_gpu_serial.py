@@ -196,12 +196,15 @@ def test_serial_chain_full_size(scene, w, h, spp):
 
 def test_serial_chain_check_sees_a_corrupted_state(monkeypatch):
     """The check is not vacuous: one corrupted start state breaks the link
-    into that sample and the link out of it (sample 0: the seed link)."""
+    into that sample and the link out of it (sample 0: the seed link).  The
+    hook corrupts a scratch copy only the check reads: the frame is still the
+    reference's."""
     src = scene_text("world.txt")
     world = R.World(src)
-    _, st = world.render(40, 30, 4, 8, mode=R.RNG_SERIAL, serial_check=True)
+    good, st = world.render(40, 30, 4, 8, mode=R.RNG_SERIAL, serial_check=True)
     assert st["serial_chain_breaks"] == 0
     for j, want in ((777, 2), (0, 2), (40 * 30 * 4 - 1, 2)):
         monkeypatch.setenv("RT_AMD_SERIAL_BREAK", str(j))
-        _, st = world.render(40, 30, 4, 8, mode=R.RNG_SERIAL, serial_check=True)
+        out, st = world.render(40, 30, 4, 8, mode=R.RNG_SERIAL, serial_check=True)
         assert st["serial_chain_breaks"] == want, (j, st["serial_chain_breaks"])
+        assert_bits_equal(out, good, "frame under the check's test hook")

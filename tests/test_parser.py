@@ -5,6 +5,8 @@ Every parsed float, camera vector and material must be bit-identical, and
 every rejected input must fail with the same ParseError kind (parser.rs:11-18;
 100 = an input on which the reference panics).  No GPU needed.
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -123,6 +125,40 @@ def _unicode_alnum_truth():
         alpha = bisect.bisect_right(inv, c) % 2 == 1
         return alpha or unicodedata.category(chr(c)) in ("Nd", "Nl", "No")
     return truth, inv
+
+
+def _read_ranges(path, name):
+    """(lo, hi) pairs of a generated C++ range table."""
+    import re
+
+    text = open(path).read()
+    body = text.split(name + "[][2] = {", 1)[1].split("};", 1)[0]
+    return [(int(a, 16), int(b, 16)) for a, b in re.findall(r"\{0x([0-9A-F]+), 0x([0-9A-F]+)\}", body)]
+
+
+def test_oracle_and_product_identifier_tables_built_apart_agree():
+    """The oracle's is_alphanumeric table (oracle/gen_alnum.pl: perl's regex
+    engine per code point, built into oracle/build/) and the product's
+    (tools/gen_unicode_alnum.py: perl's Alpha/Y.pl inversion list + Python's
+    unicodedata) come from separate generators; they must agree range for
+    range, and with the Unicode sources at every range edge."""
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    oracle_h = os.path.join(root, "oracle", "build", "alnum_oracle.h")
+    product_h = os.path.join(root, "rust-swift-raytracer_amd", "csrc", "unicode_alnum.h")
+    if not os.path.exists(oracle_h):
+        pytest.skip("oracle not built (make -C oracle)")
+    src = open(os.path.join(root, "oracle", "rt_oracle.cpp")).read()
+    assert "#include \"../rust-swift-raytracer_amd" not in src, "the oracle must not include product headers"
+    ours = _read_ranges(product_h, "kAlnumRanges")
+    theirs = _read_ranges(oracle_h, "kRanges")
+    assert len(ours) == 768 and ours == theirs
+    truth, _ = _unicode_alnum_truth()
+    for lo, hi in theirs:
+        assert truth(lo) and truth(hi)
+        if lo > 0 and not 0xD800 <= lo - 1 <= 0xDFFF:
+            assert not truth(lo - 1), hex(lo - 1)
+        if hi + 1 < 0x110000 and not 0xD800 <= hi + 1 <= 0xDFFF:
+            assert not truth(hi + 1), hex(hi + 1)
 
 
 def test_identifier_characters_follow_unicode_alphanumeric():
