@@ -399,8 +399,10 @@ def _report(args, src, world, W, H, spp, depth, st0, rays, elapsed, trace_ms, co
     out_bytes = rows * W * 4
     # roofline.traffic: HBM bytes per trace launch from the separate rocprofv3
     # --pmc FETCH_SIZE / WRITE_SIZE passes of tools/profile.sh (counters cannot
-    # be read inside this run), reported with the profiled build's sha256 next
-    # to the sha256 of the library this run loaded
+    # be read inside this run), keyed on the sha256 of the frame trace kernels'
+    # machine code (tools/kernel_hash.py) -- the code those counters describe --
+    # next to the same hash of the library this run loaded; the whole-.so
+    # hashes are reported too
     traffic, tsrc = None, None
     tfile = os.path.join(ROOT, "profiles", "hbm_traffic.json")
     if os.path.exists(tfile):
@@ -409,7 +411,14 @@ def _report(args, src, world, W, H, spp, depth, st0, rays, elapsed, trace_ms, co
         traffic = ent.get("trace_bytes_per_launch")
         with open(R.LIB_PATH, "rb") as fh:
             loaded = hashlib.sha256(fh.read()).hexdigest()
+        sys.path.insert(0, os.path.join(ROOT, "tools"))
+        import kernel_hash  # noqa: E402
+        kloaded, _ = kernel_hash.frame_kernel_hash(R.LIB_PATH)
         tsrc = {"file": "profiles/hbm_traffic.json", "profile": ent.get("from"),
+                "profiled_trace_kernel_sha256": ent.get("trace_kernel_sha256"),
+                "benched_trace_kernel_sha256": kloaded,
+                "same_trace_kernel": ent.get("trace_kernel_sha256") is not None
+                and ent.get("trace_kernel_sha256") == kloaded,
                 "profiled_lib_sha256": ent.get("lib_sha256"), "benched_lib_sha256": loaded,
                 "same_binary": ent.get("lib_sha256") == loaded}
     ms_per_step = elapsed / args.steps * 1e3

@@ -20,7 +20,14 @@ enum : uint32_t { kRngCounter = 1, kRngReplay = 2 };
 //     stream state after the frame's last sample), else 0
 //   kRngSerialCoalesce: not a trace_kernel pass -- render_frame launches the
 //     coalescing block search (launch_serial_coalesce) with the frame's scene
-enum : uint32_t { kRngSerialCount = 3, kRngSerialEstimate = 4, kRngSerialCheck = 5, kRngSerialCoalesce = 6 };
+//   kRngSerialPixel: the pixel table pass: a sample's scatter
+//     count depends only on its pixel and its start position in the stream, so
+//     the iteration's count table is gathered (launch_serial_pixtab_gather)
+//     from one trace per (pixel, stream position) its samples' windows cover:
+//     variant e of local pixel q starts at win[plo(q) + e] (ctrl[7] = the
+//     iteration's positions per pixel, set by serial_window_kernel)
+enum : uint32_t { kRngSerialCount = 3, kRngSerialEstimate = 4, kRngSerialCheck = 5, kRngSerialCoalesce = 6,
+                  kRngSerialPixel = 7 };
 enum : uint32_t { kMatDiffuse = 0, kMatMetal = 1, kMatDielectric = 2, kMatEmission = 3 };
 constexpr uint32_t kPrimaryTriStripW = 8;  // bvh.h kTriStripW
 #ifndef RT_TRACE_RING
@@ -141,6 +148,7 @@ struct TraceParams {
     uint32_t sspp;            // the frame's spp ...
     FastDiv div_sspp;         // ... and its divider
     uint32_t max_draws;       // 2 + 3 * max(depth, 0): bound of the draw count search
+    uint32_t sL, sK;          // kRngSerialPixel: the iteration length and the launch's K
 };
 
 // Candidate k of chunk sample jl (frame sample a + jl) means B = serial_lo + k
@@ -196,9 +204,22 @@ size_t serial_scan_scratch(uint32_t npix);
 // lo (optional): L u32, the iteration's window bases serial_lo(a, jl) with the
 // iteration's K (ctrl[5] when set, else K), for the count pass
 // (TraceParams::slo) and the walks.
-hipError_t launch_serial_window(const uint32_t *ctrl, const uint32_t *jump, uint32_t *win, uint32_t n,
+// pix_spp (optional, nonzero: the pixel table pass follows): also sets ctrl[7]
+// to the iteration's stream positions per pixel (serial_pixtab_span; ctrl[7]
+// must be 0 on entry: the initial block and the finish kernel leave it so).
+hipError_t launch_serial_window(uint32_t *ctrl, const uint32_t *jump, uint32_t *win, uint32_t n,
                                 SerialPred M, uint32_t *lo, uint32_t L, uint32_t K, uint32_t depth,
-                                uint32_t nserial, hipStream_t stream);
+                                uint32_t nserial, uint32_t pix_spp, hipStream_t stream);
+// The pixel table pass's result (ptab: b of local pixel q at position plo(q) + e
+// = ptab[q * ctrl[7] + e]) gathered into the count table of the iteration
+// (table[jl * K + k], the layout the walks read; -1 outside the traced span)
+hipError_t launch_serial_pixtab_gather(const uint32_t *ctrl, const float *ptab, const uint32_t *lo, float *table,
+                                       uint32_t L, uint32_t K, uint32_t spp, uint32_t nserial, hipStream_t stream);
+// the largest positions-per-pixel span an iteration can need (ptab sizing):
+// 2 (spp - 1) + 3 (depth (spp - 1) + K) + 1
+inline uint32_t serial_pixtab_emax(uint32_t spp, uint32_t K, uint32_t depth) {
+    return 2u * (spp - 1u) + 3u * (depth * (spp - 1u) + K) + 1u;
+}
 // Coalescing block search (render.hip serial_coalesce_kernel): one workgroup
 // per block of R samples of the iteration writes bend and path (layouts of
 // launch_serial_walk's block walks) by tracing each block's distinct live

@@ -531,6 +531,14 @@ __device__ __forceinline__ void tri_leaf(const TraceParams &p, F3 org, F3 dir, b
 template <bool kSerial>
 __device__ __forceinline__ void job_pixel(const TraceParams &p, uint32_t job, uint32_t &s,
                                           uint32_t &col, uint32_t &row) {
+    if (kSerial && p.mode == kRngSerialPixel) {
+        // job = local pixel q * E + position: pixel p0 + q (s is not used)
+        const uint32_t pix = fdiv(p.cbase, p.div_sspp) + fdiv(job, p.div_spp);
+        s = 0;
+        row = fdiv(pix, p.div_width);
+        col = pix - row * p.width;
+        return;
+    }
     if (kSerial) {
         // SERIAL passes: job = launch sample * V + variant; frame sample j =
         // (row * W + col) * spp + s in the reference's loop order (common.rs:327-336)
@@ -561,6 +569,18 @@ __device__ __forceinline__ uint32_t serial_start(const TraceParams &p, uint32_t 
                                             : serial_lo(p.sM, p.cbase, jl, p.spp, (p.max_draws - 2u) / 3u,
                                                         p.nserial)) + k)];
     if (p.mode == kRngSerialCheck) return p.win[p.cbase + jl];
+    if (p.mode == kRngSerialPixel) {
+        // local pixel q = jl, position plo(q) + k (kept inside the pixel's span:
+        // the launch's E is the widest pixel's)
+        const uint32_t a = p.cbase, ss = p.sspp;
+        const uint32_t ln = min(p.sL, p.nserial - a);
+        const uint32_t p0 = fdiv(a, p.div_sspp);
+        const uint32_t jf = jl == 0u ? 0u : (p0 + jl) * ss - a;
+        const uint32_t jz = min((p0 + jl + 1u) * ss - a, ln) - 1u;
+        const uint32_t plo = 2u * jf + 3u * p.slo[jf];
+        const uint32_t phi = 2u * jz + 3u * (p.slo[jz] + p.sK - 1u);
+        return p.win[min(plo + k, max(phi, plo))];
+    }
     return counter_seed(p.seed, (uint64_t)(p.cbase + jl) * p.spp + k);
 }
 
@@ -767,6 +787,19 @@ void trace_kernel(TraceParams p) {
             p.spp = K;
             p.div_spp = make_fastdiv(K);
             p.njobs = p.npix * K;
+        }
+        if (p.mode == kRngSerialPixel) {
+            // this iteration's pixels and positions per pixel (the launch was
+            // sized for their bounds): job = local pixel q * E + e
+            p.sK = K != 0u && K < p.sK ? K : p.sK;  // (serial_k)
+            const uint32_t E = min(p.ctrl[7], p.spp);
+            const uint32_t ln = min(p.sL, p.nserial - p.cbase);
+            const uint32_t p0 = fdiv(p.cbase, p.div_sspp);
+            const uint32_t npq = E ? fdiv(p.cbase + ln - 1u, p.div_sspp) - p0 + 1u : 0u;
+            p.spp = max(E, 1u);
+            p.div_spp = make_fastdiv(p.spp);
+            p.npix = npq;
+            p.njobs = npq * E;
         }
     }
     const uint32_t lane = __lane_id();
@@ -1457,12 +1490,14 @@ constexpr uint32_t kWinPerThread = 16;
 // It also tabulates the iteration's window bases lo[jl] = serial_lo(a, jl) for
 // jl < L (a = ctrl[4], K = the iteration's candidates), which the count pass
 // and the walks then load instead of evaluating M twice per step.
-__global__ __launch_bounds__(256) void serial_window_kernel(const uint32_t *__restrict__ ctrl,
+// pix_spp != 0 (the pixel table pass follows): ctrl[7] = max over the
+// iteration's pixels of the stream positions their samples' windows span.
+__global__ __launch_bounds__(256) void serial_window_kernel(uint32_t *__restrict__ ctrl,
                                                             const uint32_t *__restrict__ jump,
                                                             uint32_t *__restrict__ win, uint32_t n,
                                                             SerialPred M, uint32_t *__restrict__ lo,
                                                             uint32_t L, uint32_t Kmax, uint32_t depth,
-                                                            uint32_t nserial) {
+                                                            uint32_t nserial, uint32_t pix_spp) {
     if (ctrl[0] != 0u) return;
     if (lo != nullptr) {
         const uint32_t k = ctrl[5];
@@ -1470,6 +1505,22 @@ __global__ __launch_bounds__(256) void serial_window_kernel(const uint32_t *__re
         const uint32_t a = ctrl[4];
         for (uint32_t jl = blockIdx.x * blockDim.x + threadIdx.x; jl < L; jl += gridDim.x * blockDim.x)
             lo[jl] = serial_lo(M, a, jl, K, depth, nserial);
+        if (pix_spp != 0u) {
+            // local pixel q: samples [jf, jz] of the iteration, windows from
+            // 2 jf + 3 lo(jf) to 2 jz + 3 (lo(jz) + K - 1)
+            const uint32_t ln = min(L, nserial - a);
+            const uint32_t p0 = a / pix_spp, npq = (a + ln - 1u) / pix_spp - p0 + 1u;
+            uint32_t span = 0;
+            for (uint32_t q = blockIdx.x * blockDim.x + threadIdx.x; q < npq; q += gridDim.x * blockDim.x) {
+                const uint32_t jf = q == 0u ? 0u : (p0 + q) * pix_spp - a;
+                const uint32_t jz = min((p0 + q + 1u) * pix_spp - a, ln) - 1u;
+                const uint32_t lf = serial_lo(M, a, jf, K, depth, nserial);
+                const uint32_t lz = serial_lo(M, a, jz, K, depth, nserial);
+                const uint32_t hi = 2u * jz + 3u * (lz + K - 1u), lo0 = 2u * jf + 3u * lf;
+                span = max(span, hi >= lo0 ? hi - lo0 + 1u : 1u);
+            }
+            if (span) atomicMax(ctrl + 7, span);
+        }
     }
     // the jump matrices this workgroup's threads need (bits of i0 below 32),
     // staged in LDS: the jumps then read no global memory
@@ -1689,6 +1740,7 @@ __global__ __launch_bounds__(256) void serial_walk_finish_kernel(
         ctrl[2] += B;
         ctrl[3] += 1u;
         ctrl[4] = a + done;
+        ctrl[7] = 0u;  // (the next window kernel's pixel span, atomicMax)
         if (a + done >= nserial) ctrl[0] = 1u;
         if (V != nullptr) {
             // the next iteration's windows: +-z sigma of the scatter-count
@@ -2264,13 +2316,48 @@ hipError_t launch_serial_tables(double *tab, double *scratch, uint32_t npix, uin
     return hipGetLastError();
 }
 
-hipError_t launch_serial_window(const uint32_t *ctrl, const uint32_t *jump, uint32_t *win, uint32_t n,
+hipError_t launch_serial_window(uint32_t *ctrl, const uint32_t *jump, uint32_t *win, uint32_t n,
                                 SerialPred M, uint32_t *lo, uint32_t L, uint32_t K, uint32_t depth,
-                                uint32_t nserial, hipStream_t stream) {
+                                uint32_t nserial, uint32_t pix_spp, hipStream_t stream) {
     if (!n) return hipSuccess;
     const uint32_t threads = std::max((n + kWinPerThread - 1) / kWinPerThread, lo ? std::min(L, 1u << 16) : 0u);
     hipLaunchKernelGGL(serial_window_kernel, dim3((threads + 255) / 256), dim3(256), 0, stream, ctrl,
-                       jump, win, n, M, lo, L, K, depth, nserial);
+                       jump, win, n, M, lo, L, K, depth, nserial, pix_spp);
+    return hipGetLastError();
+}
+
+// table[jl * K + k] = b of sample jl at offset lo[jl] + k, i.e. at stream
+// position 2 jl + 3 (lo[jl] + k) of the iteration, which the pixel table pass
+// traced for the sample's pixel q at ptab[q * E + (position - plo(q))]
+__global__ __launch_bounds__(256) void serial_pixtab_gather_kernel(const uint32_t *__restrict__ ctrl,
+                                                                   const float *__restrict__ ptab,
+                                                                   const uint32_t *__restrict__ lo,
+                                                                   float *__restrict__ table, uint32_t L,
+                                                                   uint32_t Kmax, uint32_t spp, uint32_t nserial) {
+    if (ctrl[0] != 0u) return;
+    const uint32_t K = serial_k(ctrl, Kmax);
+    const uint32_t E = ctrl[7];
+    const uint32_t a = ctrl[4];
+    const uint32_t n = min(L, nserial - a);
+    const uint32_t p0 = a / spp;
+    for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < n * K; t += gridDim.x * blockDim.x) {
+        const uint32_t jl = t / K, k = t - jl * K;
+        const uint32_t q = (a + jl) / spp - p0;
+        const uint32_t jf = q == 0u ? 0u : (p0 + q) * spp - a;
+        const uint32_t plo = 2u * jf + 3u * lo[jf];
+        const uint32_t pos = 2u * jl + 3u * (lo[jl] + k);
+        // (lo is non-decreasing up to a rounding tie of the double prediction:
+        // a position outside the traced span reads as "left the window")
+        table[t] = (pos >= plo && pos - plo < E) ? ptab[(size_t)q * E + (pos - plo)] : -1.0f;
+    }
+}
+
+hipError_t launch_serial_pixtab_gather(const uint32_t *ctrl, const float *ptab, const uint32_t *lo, float *table,
+                                       uint32_t L, uint32_t K, uint32_t spp, uint32_t nserial, hipStream_t stream) {
+    const uint64_t n = (uint64_t)L * K;
+    const uint32_t blocks = (uint32_t)std::min<uint64_t>((n + 255) / 256, 4096);
+    hipLaunchKernelGGL(serial_pixtab_gather_kernel, dim3(std::max(blocks, 1u)), dim3(256), 0, stream, ctrl, ptab,
+                       lo, table, L, K, spp, nserial);
     return hipGetLastError();
 }
 

@@ -54,7 +54,7 @@ DeviceState::~DeviceState() {
                     sph_shade, sph_kind, tbvh_nodes, tbvh_tris, tbvh_loose,
                     cam_nodes, cam_tris, ptl_off, ptl_items, spl, tile, gath,
                     sstates, stab, sscan, swin, sjump, sctrl, sbend, spath, sfin,
-                    gspl, gspl_rects, gspl_flag, scheck, slo, ssbend, ssb};
+                    gspl, gspl_rects, gspl_flag, scheck, slo, ssbend, ssb, sptab};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
     for (hipEvent_t e : ev)
@@ -171,15 +171,6 @@ static int device_for(WorldState &w, int want, DeviceState *&out) {
                         fits = fits && d->blocks_per_cu_lds[c][st] > 0;
                     }
                 if (fits) d->lds_bytes = lds;
-                if (fits && !tri) {
-                    const size_t plds = pixel_lds_bytes(lp);
-                    bool pfits = true;
-                    for (int c = 0; c < 2; ++c) {
-                        HIP_TRY(pixel_occupancy(&d->blocks_per_cu_pix[c], plds, c));
-                        pfits = pfits && d->blocks_per_cu_pix[c] > 0;
-                    }
-                    if (pfits) d->pix_lds = plds;
-                }
             }
         }
         const TriangleBVH &tb = w.tbvh;
@@ -568,12 +559,7 @@ int render_frame(WorldState &w, const CameraModel &cam, size_t width, size_t hei
     const int sv = p.step ? 1 : 0;
     const bool timed = stats != nullptr;  // HIP-event timing + counters need a host wait
     const int ctv = timed ? 1 : 0;         // launch_trace runs the counting variant iff p.stats
-    // one pixel per lane (pixel_kernel): sphere-only frames with
-    // the tree in LDS and the fused resolve; RT_AMD_PIXEL=0 keeps trace_kernel
-    const bool pixmode = fused && !sp && use_bvh && p.use_lds && d->ntri == 0 && d->pix_lds > 0 &&
-                         env_u64("RT_AMD_PIXEL", 1) != 0;
-    const int bpc = pixmode    ? d->blocks_per_cu_pix[ctv]
-                    : !use_bvh  ? d->blocks_per_cu[ctv][sv]
+    const int bpc = !use_bvh   ? d->blocks_per_cu[ctv][sv]
                     : p.use_lds ? d->blocks_per_cu_lds[ctv][sv]
                                 : d->blocks_per_cu_bvh[ctv][sv];
     const uint64_t waves_per_block = trace_block_threads(use_bvh && p.use_lds, p.ntri != 0) / 64;
@@ -594,8 +580,11 @@ int render_frame(WorldState &w, const CameraModel &cam, size_t width, size_t hei
         const uint64_t njobs = (uint64_t)sp->nsamples * sp->variants;
         if (njobs == 0) return 0;
         if (njobs > 0x7FFFFFFFull) { set_error("serial pass too large"); return -1; }
-        if (sp->mode != kRngSerialCoalesce) HIP_TRY(grow(d->samples, d->samples_cap, 3 * njobs));
-        p.samples = d->samples;
+        if (sp->mode != kRngSerialCoalesce && sp->mode != kRngSerialPixel)
+            HIP_TRY(grow(d->samples, d->samples_cap, 3 * njobs));
+        p.samples = sp->mode == kRngSerialPixel ? sp->ptab : d->samples;
+        p.sL = sp->L;
+        p.sK = sp->Kmax;
         p.ring = nullptr;
         p.ring_shift = 0;
         p.mode = sp->mode;
@@ -650,35 +639,7 @@ int render_frame(WorldState &w, const CameraModel &cam, size_t width, size_t hei
         p.njobs = (uint32_t)njobs;
         p.npix = (uint32_t)(rows * width);
         if (timed) HIP_TRY(hipEventRecord(d->ev[0], s));
-        if (njobs && pixmode) {
-            // pixels per lane: >= 16 samples per lane before the grid shrinks
-            const uint64_t per_block = waves_per_block * 64;
-            uint64_t blocks = std::min<uint64_t>(full_blocks, (njobs + 16 * per_block - 1) / (16 * per_block));
-            blocks = std::max<uint64_t>(blocks, 1);
-            const uint64_t nwaves = blocks * waves_per_block;
-            const uint64_t npix = rows * width;
-            // a wave's first pull fills its lanes (or shares the launch's
-            // pixels out evenly); later pulls take up to 64
-            p.chunk0 = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(64, npix / nwaves));
-            uint64_t chunk = env_u64("RT_AMD_PIX_CHUNK", 0);
-            if (!chunk) chunk = std::max<uint64_t>(1, std::min<uint64_t>(64, npix / (2 * nwaves)));
-            p.chunk = (uint32_t)chunk;
-            uint64_t parts = env_u64("RT_AMD_PARTS", 16);
-            parts = std::max<uint64_t>(1, std::min<uint64_t>({parts, kMaxParts, npix / (16 * chunk) + 1}));
-            p.nparts = (uint32_t)parts;
-            HIP_TRY(grow(d->ring, d->ring_cap, nwaves * pixel_help_floats()));
-            HIP_TRY(grow(d->psum, d->psum_cap, npix));
-            p.ring = d->ring;
-            p.ring_shift = 0;
-            p.psum = d->psum;
-            HIP_TRY(hipMemsetAsync(d->counter, 0, parts * 128, s));
-            HIP_TRY(launch_pixel(p, (uint32_t)blocks, s));
-            d->last_jobs = 0;
-            d->last_spp = spp;
-            d->last_fused = true;
-            ++launches;
-            waves = (uint32_t)nwaves;
-        } else if (njobs) {
+        if (njobs) {
             const uint64_t jobs_per_block = waves_per_block * 256;
             uint64_t blocks = std::min<uint64_t>(full_blocks, (njobs + jobs_per_block - 1) / jobs_per_block);
             blocks = std::max<uint64_t>(blocks, 1);
@@ -730,8 +691,7 @@ int render_frame(WorldState &w, const CameraModel &cam, size_t width, size_t hei
             waves = (uint32_t)nwaves;
         }
         if (timed) HIP_TRY(hipEventRecord(d->ev[1], s));
-        if (!fused)  // (spp 0: no samples, the resolve still writes every pixel; the
-                     // pixel kernel's epilogue is part of launch_pixel)
+        if (!fused)  // (spp 0: no samples, the resolve still writes every pixel)
             HIP_TRY(launch_resolve_ex(d->samples, d_out, (uint32_t)(rows * width), spp, inv_spp,
                                       (uint32_t)width, (uint32_t)r0, s));
         if (timed) {
@@ -900,7 +860,16 @@ static int serial_find_states(WorldState &w, const CameraModel &cam, size_t widt
         // triangles), not on o.accel: a large scene forced to RT_ACCEL_BRUTE
         // has even longer traces and takes the count pass too.
         const bool trees = d->nnodes > 0 || d->tnodes > 0;
-        bool coalesce = env_u64("RT_AMD_SERIAL_COALESCE", trees ? 0 : 1) != 0 && depth < 1024;
+        // The pixel table pass (round 4, the default from 4 samples per pixel):
+        // a sample's scatter count depends only on its pixel and its start
+        // position (the samples of one pixel trace the same camera ray from
+        // the same draws), so the count table of an iteration is gathered from
+        // one trace per (pixel, stream position) that any of the pixel's
+        // samples' windows covers -- about L (3K / spp + 2 + 3 mu) traces
+        // instead of the count pass's L K, and independent ones, unlike the
+        // coalescing search's chains.  RT_AMD_SERIAL_PIXTAB=0: the searches below.
+        bool pixtab = spp >= 4 && env_u64("RT_AMD_SERIAL_PIXTAB", 0) != 0;
+        bool coalesce = !pixtab && env_u64("RT_AMD_SERIAL_COALESCE", trees ? 0 : 1) != 0 && depth < 1024;
         // (iterations of 128 k samples in blocks of 32 for the coalescing search,
         // profiles/round3_serial/coalesce_sweep*.log; 16 k for the count pass)
         const uint64_t L = std::max<uint64_t>(
@@ -966,6 +935,15 @@ static int serial_find_states(WorldState &w, const CameraModel &cam, size_t widt
         // (the coalescing workgroup keeps K candidates' u16 slots and K + depth
         // + 1 live offsets in LDS, <= 64 KB: wider windows take the count pass)
         if (K > 4096 || serial_coalesce_search_lds((uint32_t)K, depth) > 64 * 1024) coalesce = false;
+        // the pixel table's bounds: pixels an iteration touches x the widest
+        // span of positions one pixel's windows can cover
+        const uint64_t npq_max = L / spp + 2;
+        const uint64_t emax = pixtab ? serial_pixtab_emax((uint32_t)spp, (uint32_t)K, depth) : 0;
+        if (pixtab && (npq_max * emax > (1ull << 28) || emax > 0x7FFFFFFFull)) pixtab = false;
+        if (pixtab) {
+            HIP_TRY(grow(d->sptab, d->sptab_cap, npq_max * emax));
+            HIP_TRY(grow(d->samples, d->samples_cap, L * K));
+        }
         // The walks size each iteration's windows from the per-pixel variances
         // (V: prefix sums over pixels of spp var, then var; the variance of
         // samples [0, j) is PV[p] + (j - p spp) var[p]): 2 z (sqrt(V) + 0.05
@@ -1035,15 +1013,28 @@ static int serial_find_states(WorldState &w, const CameraModel &cam, size_t widt
             const auto t0 = std::chrono::steady_clock::now();
             for (uint64_t q = 0; q < it; ++q) {
                 HIP_TRY(launch_serial_window(d->sctrl, d->sjump, d->swin, (uint32_t)wlen, pred, d->slo,
-                                             (uint32_t)L, (uint32_t)K, depth, (uint32_t)N, s));
-                SerialPass sp{coalesce ? kRngSerialCoalesce : kRngSerialCount, 0u, (uint32_t)L, (uint32_t)K,
-                              d->swin, pred, d->sctrl, d->slo};
-                sp.path = d->spath;
-                sp.bend = d->sbend;
-                sp.R = (uint32_t)R_walk;
-                sp.dbg = dbg_cnt;
-                rc = render_frame(w, cam, width, height, ob, nullptr, s, nullptr, &sp);
-                if (rc) return rc;
+                                             (uint32_t)L, (uint32_t)K, depth, (uint32_t)N,
+                                             pixtab ? (uint32_t)spp : 0u, s));
+                if (pixtab) {
+                    SerialPass sp{kRngSerialPixel, 0u, (uint32_t)npq_max, (uint32_t)emax, d->swin, pred, d->sctrl,
+                                  d->slo};
+                    sp.ptab = d->sptab;
+                    sp.L = (uint32_t)L;
+                    sp.Kmax = (uint32_t)K;
+                    rc = render_frame(w, cam, width, height, ob, nullptr, s, nullptr, &sp);
+                    if (rc) return rc;
+                    HIP_TRY(launch_serial_pixtab_gather(d->sctrl, d->sptab, d->slo, d->samples, (uint32_t)L,
+                                                       (uint32_t)K, (uint32_t)spp, (uint32_t)N, s));
+                } else {
+                    SerialPass sp{coalesce ? kRngSerialCoalesce : kRngSerialCount, 0u, (uint32_t)L, (uint32_t)K,
+                                  d->swin, pred, d->sctrl, d->slo};
+                    sp.path = d->spath;
+                    sp.bend = d->sbend;
+                    sp.R = (uint32_t)R_walk;
+                    sp.dbg = dbg_cnt;
+                    rc = render_frame(w, cam, width, height, ob, nullptr, s, nullptr, &sp);
+                    if (rc) return rc;
+                }
                 HIP_TRY(launch_serial_walk(d->sctrl, coalesce ? nullptr : d->samples, pred, adapt ? Vdev : nullptr,
                                            (uint32_t)npix, (uint32_t)spp, (float)z, (float)serial_floor(spp * R),
                                            d->swin, d->sstates, d->sbend, gather ? d->spath : nullptr,
@@ -1082,7 +1073,8 @@ static int serial_find_states(WorldState &w, const CameraModel &cam, size_t widt
         if (env_u64("RT_AMD_SERIAL_DEBUG", 0)) {
             std::fprintf(stderr, "serial debug: %s N %llu L %llu R %llu K %llu sigma %.3f: %u iterations (%u "
                          "stopped short), %llu queued, estimate + tables %.1f ms, enqueue %.1f ms, wait %.1f ms\n",
-                         coalesce ? "coalesce" : "count", (unsigned long long)N, (unsigned long long)L,
+                         pixtab ? "pixel table" : coalesce ? "coalesce" : "count", (unsigned long long)N,
+                         (unsigned long long)L,
                          (unsigned long long)R_walk, (unsigned long long)K, sigma,
                          ctrl[3], ctrl[6], (unsigned long long)queued, t_prep, t_enqueue, t_wait);
         }

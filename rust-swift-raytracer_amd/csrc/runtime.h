@@ -78,6 +78,7 @@ struct DeviceState {
     uint32_t *swin = nullptr;        size_t swin_cap = 0;
     uint32_t *sbend = nullptr;       size_t sbend_cap = 0;
     uint32_t *spath = nullptr;       size_t spath_cap = 0;  // block walks' paths (L x K)
+    float *sptab = nullptr;          size_t sptab_cap = 0;  // pixel table pass: b per (pixel, position)
     uint32_t *sfin = nullptr;                               // chain result (4 + kMaxWalkBlocks)
     uint32_t *sjump = nullptr;
     uint32_t *sctrl = nullptr;
@@ -138,6 +139,10 @@ struct SerialPass {
     uint32_t *path = nullptr, *bend = nullptr;
     uint32_t R = 0;
     unsigned long long *dbg = nullptr;  // (RT_AMD_SERIAL_DEBUG: launch_serial_coalesce's counters)
+    // kRngSerialPixel: the table it writes (nsamples pixels x variants
+    // positions, the launch's bounds), the iteration length and its K
+    float *ptab = nullptr;
+    uint32_t L = 0, Kmax = 0;
 };
 
 // Renders rank's tile of a width x height frame into device memory d_out

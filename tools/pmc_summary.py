@@ -33,10 +33,11 @@ def short(name):
 def main(src, dst, config="c2"):
     os.makedirs(dst, exist_ok=True)
     out = {"source": os.path.basename(src.rstrip("/")), "kernels": {}}
-    sha = os.path.join(src, "lib_sha256.txt")
-    if os.path.exists(sha):
-        out["lib_sha256"] = open(sha).read().strip()
-        shutil.copy(sha, os.path.join(dst, "lib_sha256.txt"))
+    for key in ("lib_sha256", "kernel_sha256"):
+        sha = os.path.join(src, key + ".txt")
+        if os.path.exists(sha):
+            out[key] = open(sha).read().strip()
+            shutil.copy(sha, os.path.join(dst, key + ".txt"))
     stats = glob.glob(os.path.join(src, "trace", "*kernel_stats.csv"))
     if stats:
         shutil.copy(stats[0], os.path.join(dst, "kernel_stats.csv"))
@@ -66,7 +67,8 @@ def main(src, dst, config="c2"):
         allc = json.load(open(path)) if os.path.exists(path) else {}
         allc[config] = {"trace_bytes_per_launch": tr["hbm_bytes_per_launch"],
                         "from": os.path.relpath(dst, os.path.dirname(path)),
-                        "lib_sha256": out.get("lib_sha256")}
+                        "lib_sha256": out.get("lib_sha256"),
+                        "trace_kernel_sha256": out.get("kernel_sha256")}
         with open(path, "w") as fh:
             json.dump(allc, fh, indent=1)
     print(json.dumps(out, indent=1))

@@ -8,6 +8,9 @@ OUT="$REPO/gpurun_out/prof_$TAG"
 mkdir -p "$OUT"
 # the binary these counters describe (bench.py compares it with the one it loads)
 sha256sum "$REPO/rust-swift-raytracer_amd/lib/libraytracer.so" | cut -d' ' -f1 > "$OUT/lib_sha256.txt"
+# ... and the hash of the frame trace kernels' machine code (tools/kernel_hash.py),
+# which unrelated edits to the library do not change
+python3 "$REPO/tools/kernel_hash.py" | head -1 > "$OUT/kernel_sha256.txt"
 cd /tmp && export TMPDIR=/tmp
 run() {  # run <name> <secs> <rocprof args...>
     local name=$1 secs=$2; shift 2
