@@ -560,6 +560,20 @@ __device__ __forceinline__ void job_pixel(const TraceParams &p, uint32_t job, ui
     row = p.height - 1u - ir;
 }
 
+// kRngSerialPixel: the stream positions (window indices) local pixel q's
+// samples' windows cover: from 2 jf + 3 lo(jf) to 2 jz + 3 (lo(jz) + K - 1),
+// jf / jz its first / last sample in the iteration
+__device__ __forceinline__ void serial_pixel_span(const TraceParams &p, uint32_t q, uint32_t &plo,
+                                                  uint32_t &phi) {
+    const uint32_t a = p.cbase, ss = p.sspp;
+    const uint32_t ln = min(p.sL, p.nserial - a);
+    const uint32_t p0 = fdiv(a, p.div_sspp);
+    const uint32_t jf = q == 0u ? 0u : (p0 + q) * ss - a;
+    const uint32_t jz = min((p0 + q + 1u) * ss - a, ln) - 1u;
+    plo = 2u * jf + 3u * p.slo[jf];
+    phi = 2u * jz + 3u * (p.slo[jz] + p.sK - 1u);
+}
+
 // SERIAL passes: the start state of job (launch sample jl, variant k).
 __device__ __forceinline__ uint32_t serial_start(const TraceParams &p, uint32_t job) {
     const uint32_t jl = fdiv(job, p.div_spp);
@@ -571,17 +585,21 @@ __device__ __forceinline__ uint32_t serial_start(const TraceParams &p, uint32_t 
     if (p.mode == kRngSerialCheck) return p.win[p.cbase + jl];
     if (p.mode == kRngSerialPixel) {
         // local pixel q = jl, position plo(q) + k (kept inside the pixel's span:
-        // the launch's E is the widest pixel's)
-        const uint32_t a = p.cbase, ss = p.sspp;
-        const uint32_t ln = min(p.sL, p.nserial - a);
-        const uint32_t p0 = fdiv(a, p.div_sspp);
-        const uint32_t jf = jl == 0u ? 0u : (p0 + jl) * ss - a;
-        const uint32_t jz = min((p0 + jl + 1u) * ss - a, ln) - 1u;
-        const uint32_t plo = 2u * jf + 3u * p.slo[jf];
-        const uint32_t phi = 2u * jz + 3u * (p.slo[jz] + p.sK - 1u);
+        // the launch's E is the widest pixel's; jobs past a narrower pixel's
+        // span are not traced, serial_pixel_job)
+        uint32_t plo, phi;
+        serial_pixel_span(p, jl, plo, phi);
         return p.win[min(plo + k, max(phi, plo))];
     }
     return counter_seed(p.seed, (uint64_t)(p.cbase + jl) * p.spp + k);
+}
+
+// kRngSerialPixel: false for a job past its pixel's span (the lane stays idle)
+__device__ __forceinline__ bool serial_pixel_job(const TraceParams &p, uint32_t job) {
+    const uint32_t q = fdiv(job, p.div_spp);
+    uint32_t plo, phi;
+    serial_pixel_span(p, q, plo, phi);
+    return plo + (job - q * p.spp) <= phi;
 }
 
 // Primary ray against its pixel strip's candidate records (bvh.h
@@ -810,6 +828,7 @@ void trace_kernel(TraceParams p) {
     F3 org = f3(0, 0, 0), dir = f3(0, 0, 0), inv = f3(0, 0, 0);
     float thr_r = 1.0f, thr_g = 1.0f, thr_b = 1.0f;  // ray_color's final_color
     uint32_t rng = 0, slot = ~0u, bounce = 0;  // slot ~0: no finished sample to count
+    uint32_t nscat = 0;  // (kSerial) the sample's diffuse/metal scatters so far
     uint32_t spl0 = 0, spl1 = kSphListWalk << 16;  // the pixel's primary sphere list (p.spl)
     // lane state between loop iterations (see the bounce loop below)
     enum : uint32_t { kSetup = 0, kSph = 1, kTriInit = 2, kTri = 3, kShade = 4 };
@@ -1063,6 +1082,7 @@ void trace_kernel(TraceParams p) {
                     F3 v = nrm;
                     if (kind == kMatDiffuse || kind == kMatMetal) {
                         const F3 ru = draw_unit(rng);
+                        if (kSerial) ++nscat;
                         if (kind == kMatDiffuse) {  // materials.rs:42-52
                             v = nrm + ru;
                             const float eps = 1e-8f;
@@ -1113,17 +1133,10 @@ void trace_kernel(TraceParams p) {
                     out_r = rng == (j + 1u < p.nserial ? p.win[j + 1u] : p.seed) ? 0.0f : 1.0f;
                 } else if (kSerial) {
                     // SERIAL passes: the sample's scatter count b instead of its
-                    // colour -- the draws it consumed (2 + 3b, common.rs:335-336 and
-                    // random_unit_sphere per diffuse/metal scatter, common.rs:32-38)
-                    // are the steps from its start state to its end state
-                    uint32_t x = serial_start(p, slot), n = 0;
-                    while (x != rng && n < p.max_draws) {
-                        x ^= x << 13;
-                        x ^= x >> 17;
-                        x ^= x << 5;
-                        ++n;
-                    }
-                    out_r = (x == rng && n >= 2u) ? (float)((n - 2u) / 3u) : -1.0f;
+                    // colour -- it drew 2 + 3b numbers (common.rs:335-336 and one
+                    // random_unit_sphere per diffuse/metal scatter, common.rs:32-38),
+                    // counted as they were drawn
+                    out_r = (float)nscat;
                 }
                 // planar (R, G, B planes): 12 B per sample, to the slab or the
                 // ring (SERIAL passes: plane 0 only)
@@ -1228,8 +1241,11 @@ void trace_kernel(TraceParams p) {
                 uint32_t s, col, row;
                 job_pixel<kSerial>(p, job, s, col, row);
                 slot = job + cur_off;
+                bool take = true;
                 if (kSerial) {
+                    nscat = 0;
                     rng = serial_start(p, job);
+                    if (p.mode == kRngSerialPixel) take = serial_pixel_job(p, job);
                 } else {
                     const uint64_t gjob = ((uint64_t)row * p.width + col) * p.spp + s;
                     rng = (p.mode == kRngReplay) ? p.replay[gjob] : counter_seed(p.seed, gjob);
@@ -1267,7 +1283,7 @@ void trace_kernel(TraceParams p) {
                 thr_r = thr_g = thr_b = 1.0f;
                 bounce = 0;
                 phase = kSetup;
-                active = true;
+                active = take;
             }
             pool_next += min(ndead, avail);
             // ask for the next chunk now; the reply is only waited for when the

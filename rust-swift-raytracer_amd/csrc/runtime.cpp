@@ -612,6 +612,10 @@ int render_frame(WorldState &w, const CameraModel &cam, size_t width, size_t hei
         uint64_t chunk = std::min<uint64_t>(256, std::max<uint64_t>(64, njobs / (nwaves * 16) / 64 * 64));
         chunk = chunk >= sp->variants ? chunk / sp->variants * sp->variants : sp->variants;
         if (sp->mode == kRngSerialCount) chunk = env_u64("RT_AMD_SERIAL_CCHUNK", 128);
+        // the pixel table pass: chunks of consecutive positions of one pixel, not
+        // whole pixels (a pixel's span is 10^3 positions: whole-pixel chunks
+        // left most waves without work)
+        if (sp->mode == kRngSerialPixel) chunk = env_u64("RT_AMD_SERIAL_PCHUNK", 64);
         p.chunk = (uint32_t)std::max<uint64_t>(1, chunk);
         uint64_t parts = std::max<uint64_t>(
             1, std::min<uint64_t>({(uint64_t)(p.step ? 64 : 16), kMaxParts, njobs / (16 * chunk) + 1}));
@@ -868,12 +872,22 @@ static int serial_find_states(WorldState &w, const CameraModel &cam, size_t widt
         // samples' windows covers -- about L (3K / spp + 2 + 3 mu) traces
         // instead of the count pass's L K, and independent ones, unlike the
         // coalescing search's chains.  RT_AMD_SERIAL_PIXTAB=0: the searches below.
-        bool pixtab = spp >= 4 && env_u64("RT_AMD_SERIAL_PIXTAB", 0) != 0;
+        bool pixtab = spp >= 4 && env_u64("RT_AMD_SERIAL_PIXTAB", 1) != 0;
         bool coalesce = !pixtab && env_u64("RT_AMD_SERIAL_COALESCE", trees ? 0 : 1) != 0 && depth < 1024;
         // (iterations of 128 k samples in blocks of 32 for the coalescing search,
-        // profiles/round3_serial/coalesce_sweep*.log; 16 k for the count pass)
-        const uint64_t L = std::max<uint64_t>(
-            1, std::min<uint64_t>(env_u64("RT_AMD_SERIAL_CHUNK", coalesce ? 131072 : 16384), N));
+        // profiles/round3_serial/coalesce_sweep*.log; 16 k for the count pass;
+        // the pixel table: 32 k at 16 spp, x sqrt(spp / 16) in powers of two --
+        // its traces per sample grow as K / spp ~ sqrt(L) / spp, its fixed cost
+        // per iteration as 1 / L; profiles/round4_serial/pixtab_sweep*.log:
+        // world.txt 960x540x16 16 k / 32 k / 64 k -> 141 / 114 / 121 ms, RTOW
+        // 1920x1080x64 64 k / 128 k / 256 k -> 1.01 / 1.07 / 1.24 s)
+        uint64_t Ldef = coalesce ? 131072 : 16384;
+        if (pixtab) {
+            Ldef = 32768;
+            for (uint64_t q = 64; q <= spp; q *= 4) Ldef *= 2;        // 64 spp: 64 k, 256 spp: 128 k
+            for (uint64_t q = spp; q < 16 && Ldef > 8192; q *= 4) Ldef /= 2;  // 4 spp: 16 k
+        }
+        const uint64_t L = std::max<uint64_t>(1, std::min<uint64_t>(env_u64("RT_AMD_SERIAL_CHUNK", Ldef), N));
         // windows are sized for the deviation over Lw samples (default L; a
         // longer Lw widens them, a shorter iteration stops less often)
         const uint64_t Lw = std::max<uint64_t>(1, env_u64("RT_AMD_SERIAL_WLEN", L));
@@ -962,6 +976,8 @@ static int serial_find_states(WorldState &w, const CameraModel &cam, size_t widt
         // <= kMaxWalkBlocks blocks per iteration)
         const uint64_t R_walk =
             coalesce ? std::min<uint64_t>(L, std::max<uint64_t>({env_u64("RT_AMD_SERIAL_R", 32), 1,
+                                                                 (L + kMaxWalkBlocks - 1) / kMaxWalkBlocks}))
+            : pixtab ? std::min<uint64_t>(L, std::max<uint64_t>({env_u64("RT_AMD_SERIAL_WALKR", 64), 1,
                                                                  (L + kMaxWalkBlocks - 1) / kMaxWalkBlocks}))
                      : serial_walk_block((uint32_t)L);
         uint32_t K0 = 0;  // the first iteration's candidates (later ones: the walks)

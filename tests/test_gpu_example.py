@@ -92,3 +92,24 @@ def test_emission_in_the_sphere_bvh():
         assert st["rays"] == ost["rays"]
     with pytest.raises(ValueError):
         world.set_material(n, 3, (1.0, 1.0, 1.0))
+
+
+@pytest.mark.parametrize("search", ["pixtab", "count", "coalesce"])
+def test_emission_serial_every_search(monkeypatch, search):
+    """render()'s mode (SERIAL) with emitters -- the branch that ends a path
+    with no draw (materials.rs:100-102) -- beside metal absorption and
+    dielectrics (the c_raytracer world), through each start-state search: the
+    pixel table, the count pass and the coalescing search must find the states
+    of the reference's one stream (oracle SERIAL) for every material branch."""
+    env = {"pixtab": dict(RT_AMD_SERIAL_PIXTAB="1"),
+           "count": dict(RT_AMD_SERIAL_PIXTAB="0", RT_AMD_SERIAL_COALESCE="0"),
+           "coalesce": dict(RT_AMD_SERIAL_PIXTAB="0", RT_AMD_SERIAL_COALESCE="1")}[search]
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    src = scene_text("c_raytracer_world.txt")
+    world, ref = _emissive(src, [(4, (4.0, 3.5, 3.0)), (1, (0.0, 0.9, 2.0))], [(1, (1.5, 0.25, 0.5))])
+    w, h, spp, depth = 48, 27, 8, 8
+    img, st, _ = ref.render(w, h, spp, depth, mode=O.RNG_SERIAL)
+    out, gst = world.render(w, h, spp, depth, mode=R.RNG_SERIAL, serial_check=True)
+    assert_bits_equal(out, img, f"emissive SERIAL frame ({search})")
+    assert gst["rays"] == st["rays"] and gst["serial_chain_breaks"] == 0

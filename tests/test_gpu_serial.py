@@ -80,8 +80,9 @@ def test_serial_narrow_windows_and_short_iterations(monkeypatch):
         (dict(RT_AMD_SERIAL_ADAPT="0", RT_AMD_SERIAL_CHUNK="700"), "world.txt", (33, 17, 3, 8)),
         # resolved states re-walked per block instead of gathered from the block
         # paths (the count pass: the coalescing search always gathers)
-        (dict(RT_AMD_SERIAL_GATHER="0", RT_AMD_SERIAL_COALESCE="0"), "c_raytracer_world.txt", (40, 30, 16, 8)),
-        (dict(RT_AMD_SERIAL_GATHER="0", RT_AMD_SERIAL_COALESCE="0", RT_AMD_SERIAL_K="24",
+        (dict(RT_AMD_SERIAL_GATHER="0", RT_AMD_SERIAL_COALESCE="0", RT_AMD_SERIAL_PIXTAB="0"),
+         "c_raytracer_world.txt", (40, 30, 16, 8)),
+        (dict(RT_AMD_SERIAL_GATHER="0", RT_AMD_SERIAL_COALESCE="0", RT_AMD_SERIAL_PIXTAB="0", RT_AMD_SERIAL_K="24",
               RT_AMD_SERIAL_CHUNK="300"), "world.txt", (29, 13, 4, 8)),
         (dict(RT_AMD_SERIAL_CHUNK="1"), "world.txt", (12, 9, 2, 8)),
         (dict(RT_AMD_SERIAL_CHUNK="100"), "world.txt", (13, 7, 3, 8)),
@@ -90,13 +91,23 @@ def test_serial_narrow_windows_and_short_iterations(monkeypatch):
         (dict(RT_AMD_SERIAL_CHUNK="37"), "world.txt", (15, 9, 3, 1)),
         (dict(RT_AMD_SERIAL_CHUNK="61", RT_AMD_SERIAL_K="4"), "world.txt", (15, 9, 3, 1)),
         # count-pass scheduling: small chunks of any size, many partitions
-        (dict(RT_AMD_SERIAL_COALESCE="0", RT_AMD_SERIAL_CCHUNK="37", RT_AMD_SERIAL_PARTS="256"),
-         "c_raytracer_world.txt", (40, 30, 16, 8)),
+        (dict(RT_AMD_SERIAL_COALESCE="0", RT_AMD_SERIAL_PIXTAB="0", RT_AMD_SERIAL_CCHUNK="37",
+              RT_AMD_SERIAL_PARTS="256"), "c_raytracer_world.txt", (40, 30, 16, 8)),
         # coalescing search: blocks of 1 and 7 samples, narrow windows in long blocks
-        (dict(RT_AMD_SERIAL_R="1", RT_AMD_SERIAL_CHUNK="300"), "c_raytracer_world.txt", (20, 15, 4, 8)),
-        (dict(RT_AMD_SERIAL_R="7", RT_AMD_SERIAL_CHUNK="1000"), "world.txt", (33, 17, 3, 8)),
-        (dict(RT_AMD_SERIAL_R="200", RT_AMD_SERIAL_K="24", RT_AMD_SERIAL_CHUNK="4000"), "world.txt",
-         (40, 30, 4, 8)),
+        (dict(RT_AMD_SERIAL_PIXTAB="0", RT_AMD_SERIAL_R="1", RT_AMD_SERIAL_CHUNK="300"), "c_raytracer_world.txt",
+         (20, 15, 4, 8)),
+        (dict(RT_AMD_SERIAL_PIXTAB="0", RT_AMD_SERIAL_R="7", RT_AMD_SERIAL_CHUNK="1000"), "world.txt",
+         (33, 17, 3, 8)),
+        (dict(RT_AMD_SERIAL_PIXTAB="0", RT_AMD_SERIAL_R="200", RT_AMD_SERIAL_K="24", RT_AMD_SERIAL_CHUNK="4000"),
+         "world.txt", (40, 30, 4, 8)),
+        # pixel table: odd chunks of positions, odd walk blocks, narrow windows,
+        # iterations shorter than a pixel, pixels wider than the iteration
+        (dict(RT_AMD_SERIAL_PCHUNK="7", RT_AMD_SERIAL_WALKR="5"), "c_raytracer_world.txt", (40, 30, 16, 8)),
+        (dict(RT_AMD_SERIAL_K="24", RT_AMD_SERIAL_CHUNK="512", RT_AMD_SERIAL_WALKR="33"), "c_raytracer_world.txt",
+         (80, 60, 16, 8)),
+        (dict(RT_AMD_SERIAL_CHUNK="9"), "world.txt", (13, 7, 16, 8)),
+        (dict(RT_AMD_SERIAL_CHUNK="50", RT_AMD_SERIAL_K="8"), "world.txt", (7, 5, 33, 4)),
+        (dict(RT_AMD_SERIAL_PCHUNK="1000"), "world.txt", (33, 17, 5, 8)),
     ]:
         for k, v in env.items():
             monkeypatch.setenv(k, v)
@@ -107,13 +118,22 @@ def test_serial_narrow_windows_and_short_iterations(monkeypatch):
             monkeypatch.delenv(k)
 
 
-@pytest.mark.parametrize("coalesce", ["0", "1"])
-def test_serial_search_modes(monkeypatch, coalesce):
-    """Both start-state searches on every scene family: the count pass + block
-    walks and the coalescing block search (runtime.cpp picks coalescing for
-    brute-force scenes, the count pass where trees exist), on small scenes,
+SEARCHES = {
+    # runtime.cpp serial_find_states: the pixel table (default from 4 spp), the
+    # count pass + block walks, the coalescing block search
+    "pixtab": dict(RT_AMD_SERIAL_PIXTAB="1"),
+    "count": dict(RT_AMD_SERIAL_PIXTAB="0", RT_AMD_SERIAL_COALESCE="0"),
+    "coalesce": dict(RT_AMD_SERIAL_PIXTAB="0", RT_AMD_SERIAL_COALESCE="1"),
+}
+
+
+@pytest.mark.parametrize("search", sorted(SEARCHES))
+def test_serial_search_modes(monkeypatch, search):
+    """Every start-state search on every scene family: the pixel table, the
+    count pass + block walks and the coalescing block search, on small scenes,
     the sphere tree and triangle trees, with wide and narrow windows."""
-    monkeypatch.setenv("RT_AMD_SERIAL_COALESCE", coalesce)
+    for k, v in SEARCHES[search].items():
+        monkeypatch.setenv(k, v)
     for src, size, env in [
         (scene_text("c_raytracer_world.txt"), (64, 48, 8, 8), {}),
         (scene_text("world.txt"), (48, 27, 16, 8), dict(RT_AMD_SERIAL_K="30", RT_AMD_SERIAL_CHUNK="2000")),
@@ -123,7 +143,7 @@ def test_serial_search_modes(monkeypatch, coalesce):
         for k, v in env.items():
             monkeypatch.setenv(k, v)
         img, st, out, gst, _ = _serial_pair(src, *size)
-        assert_bits_equal(out, img, f"SERIAL frame, coalesce={coalesce} {env}")
+        assert_bits_equal(out, img, f"SERIAL frame, search={search} {env}")
         assert gst["rays"] == st["rays"]
         for k in env:
             monkeypatch.delenv(k)

@@ -7,7 +7,8 @@ unrelated edit (a SERIAL kernel, host code) flip `same_binary`; this hashes
 only what the counters describe: the gfx950 code of the lean frame variants
 of trace_kernel (render.hip trace_kernel<..., kCount = false, kSerial =
 false>), i.e. the bytes of each such function symbol plus its kernel
-descriptor, taken from the clang offload bundle in the .hip_fatbin section.
+descriptor (less its position-dependent code-entry offset), taken from the
+clang offload bundle in the .hip_fatbin section.
 
   python tools/kernel_hash.py [lib.so]      -> prints the hash and the symbols
 """
@@ -75,9 +76,16 @@ def frame_kernel_hash(lib=LIB):
         return None, []
     h = hashlib.sha256()
     for n in names:
-        for part in (n, n + ".kd"):
-            h.update(part.encode())
-            h.update(syms.get(part, b""))
+        h.update(n.encode())
+        h.update(syms[n])
+        # the kernel descriptor (register counts, LDS / scratch / kernarg sizes)
+        # without kernel_code_entry_byte_offset (bytes 16-23): that field is the
+        # distance from the descriptor to the code, which moves whenever any
+        # other kernel of the library changes size
+        kd = bytearray(syms.get(n + ".kd", b""))
+        if len(kd) >= 24:
+            kd[16:24] = bytes(8)
+        h.update(bytes(kd))
     return h.hexdigest(), names
 
 
