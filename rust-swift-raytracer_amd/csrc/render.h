@@ -207,9 +207,12 @@ size_t serial_scan_scratch(uint32_t npix);
 // pix_spp (optional, nonzero: the pixel table pass follows): also sets ctrl[7]
 // to the iteration's stream positions per pixel (serial_pixtab_span; ctrl[7]
 // must be 0 on entry: the initial block and the finish kernel leave it so).
+// counters (optional): ncounters job-queue counters (32 u32 apart) the next
+// trace pass uses, zeroed here instead of by a fill launch.
 hipError_t launch_serial_window(uint32_t *ctrl, const uint32_t *jump, uint32_t *win, uint32_t n,
                                 SerialPred M, uint32_t *lo, uint32_t L, uint32_t K, uint32_t depth,
-                                uint32_t nserial, uint32_t pix_spp, hipStream_t stream);
+                                uint32_t nserial, uint32_t pix_spp, uint32_t *counters, uint32_t ncounters,
+                                hipStream_t stream);
 // The pixel table pass's result (ptab: b of local pixel q at position plo(q) + e
 // = ptab[q * ctrl[7] + e]) gathered into the count table of the iteration
 // (table[jl * K + k], the layout the walks read; -1 outside the traced span)
@@ -251,11 +254,15 @@ constexpr uint32_t kMaxWalkBlocks = 4096;  // blocks per iteration (the finish k
 // the walk sets the next iteration's candidates per sample in ctrl[5] (<= K):
 // 2 z (sqrt(V over Lw samples) + sfloor sqrt(Lw)) + 2 depth + 2; the count
 // pass and the walks use ctrl[5] when it is set.
+// ptab (optional, with path and fin): the pixel table pass's table (ptab[q *
+// ctrl[7] + e], render.h kRngSerialPixel) read by the block walks directly;
+// table is then unused.
 hipError_t launch_serial_walk(uint32_t *ctrl, const float *table, SerialPred M, const double *V,
                               uint32_t npix, uint32_t spp, float z, float sfloor, const uint32_t *win,
                               uint32_t *states, uint32_t *bend, uint32_t *path, uint32_t *fin,
                               const uint32_t *lo, uint32_t *sbend, uint32_t *sB, uint32_t L, uint32_t Lw,
-                              uint32_t K, uint32_t R, uint32_t depth, uint32_t nserial, hipStream_t stream);
+                              uint32_t K, uint32_t R, uint32_t depth, uint32_t nserial, const float *ptab,
+                              hipStream_t stream);
 // (lo: required; sbend, sB: scratch of serial_super_words(L, K, R) and ceil(L / R) K
 // u32 for the superblock chain)
 uint32_t serial_super_words(uint32_t L, uint32_t K, uint32_t R);

@@ -1513,8 +1513,12 @@ __global__ __launch_bounds__(256) void serial_window_kernel(uint32_t *__restrict
                                                             uint32_t *__restrict__ win, uint32_t n,
                                                             SerialPred M, uint32_t *__restrict__ lo,
                                                             uint32_t L, uint32_t Kmax, uint32_t depth,
-                                                            uint32_t nserial, uint32_t pix_spp) {
+                                                            uint32_t nserial, uint32_t pix_spp,
+                                                            uint32_t *__restrict__ counters, uint32_t ncounters) {
     if (ctrl[0] != 0u) return;
+    // the following trace pass's job counters (instead of a fill launch)
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < ncounters; i += gridDim.x * blockDim.x)
+        counters[32u * i] = 0u;
     if (lo != nullptr) {
         const uint32_t k = ctrl[5];
         const uint32_t K = k != 0u && k < Kmax ? k : Kmax;  // (serial_k)
@@ -1591,10 +1595,15 @@ __device__ __forceinline__ uint32_t serial_k(const uint32_t *ctrl, uint32_t K) {
 // path (optional): the offset B at the start of each of the block's samples,
 // sample-major (path[(jl - j0) * nb * K + t], coalesced), so that the states
 // of the true path are a gather (serial_states_kernel), not a re-walk
+// ptab (the pixel table pass, kRngSerialPixel): b is read from the traced
+// (pixel, position) table itself -- b of sample jl at offset B is
+// ptab[q E + (2 jl + 3 B - plo(q))], q its local pixel -- instead of a
+// gathered L x K count table (a 16 MB table instead of an 80 MB one at 32 k x
+// 617, and no gather pass); ppix: the frame's spp as a divider.
 __global__ __launch_bounds__(256) void serial_walk_blocks_kernel(
     const uint32_t *__restrict__ ctrl, const float *__restrict__ table, SerialPred M,
     uint32_t *__restrict__ bend, uint32_t *__restrict__ path, const uint32_t *__restrict__ lo, uint32_t L,
-    uint32_t K, uint32_t R, uint32_t depth, uint32_t nserial) {
+    uint32_t K, uint32_t R, uint32_t depth, uint32_t nserial, const float *__restrict__ ptab, FastDiv ppix) {
     if (ctrl[0] != 0u) return;
     K = serial_k(ctrl, K);
     const uint32_t a = ctrl[4];
@@ -1607,12 +1616,36 @@ __global__ __launch_bounds__(256) void serial_walk_blocks_kernel(
     const size_t stride = (size_t)nb * K;
     uint32_t B = (lo ? lo[j0] : serial_lo(M, a, j0, K, depth, nserial)) + k0;
     uint32_t jl = j0;
+    if (ptab != nullptr) {
+        const uint32_t E = ctrl[7], spp = ppix.d;
+        const uint32_t p0 = fastdiv_apply(a, ppix);
+        uint32_t q = fastdiv_apply(a + j0, ppix) - p0;  // local pixel of sample jl
+        uint32_t jf = q == 0u ? 0u : (p0 + q) * spp - a;  // its first sample in the iteration
+        uint32_t jnext = (p0 + q + 1u) * spp - a;        // the next pixel's
+        uint32_t plo = 2u * jf + 3u * lo[jf];
+        for (; jl < j1; ++jl) {
+            if (path) path[(size_t)(jl - j0) * stride + t] = B;
+            if (jl == jnext) {
+                ++q;
+                plo = 2u * jnext + 3u * lo[jnext];
+                jnext += spp;
+            }
+            const uint32_t l = lo[jl];
+            const uint32_t pos = 2u * jl + 3u * B;
+            const float b = (B >= l && B - l < K && pos >= plo && pos - plo < E)
+                                ? ptab[(size_t)q * E + (pos - plo)]
+                                : -1.0f;
+            if (!(b >= 0.0f)) break;
+            B += (uint32_t)b;
+        }
+    } else {
 #pragma unroll 4
-    for (; jl < j1; ++jl) {
-        if (path) path[(size_t)(jl - j0) * stride + t] = B;
-        const uint32_t nB = walk_step(table, M, a, K, depth, nserial, jl, B, lo);
-        if (nB == kWalkInvalid) break;
-        B = nB;
+        for (; jl < j1; ++jl) {
+            if (path) path[(size_t)(jl - j0) * stride + t] = B;
+            const uint32_t nB = walk_step(table, M, a, K, depth, nserial, jl, B, lo);
+            if (nB == kWalkInvalid) break;
+            B = nB;
+        }
     }
     // the block's end offset, or kWalkLeft | the samples whose end was found
     // (the path then holds the start offset of the sample that left)
@@ -2334,11 +2367,12 @@ hipError_t launch_serial_tables(double *tab, double *scratch, uint32_t npix, uin
 
 hipError_t launch_serial_window(uint32_t *ctrl, const uint32_t *jump, uint32_t *win, uint32_t n,
                                 SerialPred M, uint32_t *lo, uint32_t L, uint32_t K, uint32_t depth,
-                                uint32_t nserial, uint32_t pix_spp, hipStream_t stream) {
+                                uint32_t nserial, uint32_t pix_spp, uint32_t *counters, uint32_t ncounters,
+                                hipStream_t stream) {
     if (!n) return hipSuccess;
     const uint32_t threads = std::max((n + kWinPerThread - 1) / kWinPerThread, lo ? std::min(L, 1u << 16) : 0u);
     hipLaunchKernelGGL(serial_window_kernel, dim3((threads + 255) / 256), dim3(256), 0, stream, ctrl,
-                       jump, win, n, M, lo, L, K, depth, nserial, pix_spp);
+                       jump, win, n, M, lo, L, K, depth, nserial, pix_spp, counters, counters ? ncounters : 0u);
     return hipGetLastError();
 }
 
@@ -2391,17 +2425,21 @@ hipError_t launch_serial_walk(uint32_t *ctrl, const float *table, SerialPred M, 
                               uint32_t npix, uint32_t spp, float z, float sfloor, const uint32_t *win,
                               uint32_t *states, uint32_t *bend, uint32_t *path, uint32_t *fin,
                               const uint32_t *lo, uint32_t *sbend, uint32_t *sB, uint32_t L, uint32_t Lw,
-                              uint32_t K, uint32_t R, uint32_t depth, uint32_t nserial, hipStream_t stream) {
+                              uint32_t K, uint32_t R, uint32_t depth, uint32_t nserial, const float *ptab,
+                              hipStream_t stream) {
     if (!L || !R) return hipSuccess;
     const uint32_t nb = (L + R - 1) / R;
     if (nb > kMaxWalkBlocks) return hipErrorInvalidValue;
     const uint64_t nt = (uint64_t)nb * K;
     const uint64_t nst = (uint64_t)((nb + kSuperBlocks - 1) / kSuperBlocks) * K;
     if (!fin) path = nullptr;
-    if (table == nullptr && !path) return hipErrorInvalidValue;  // (the coalescing search needs the gather)
-    if (table != nullptr)
+    // (the coalescing search and the pixel table need the recorded paths: the
+    // finish kernel's lane-serial fallback reads a count table)
+    if ((table == nullptr || ptab != nullptr) && !path) return hipErrorInvalidValue;
+    if (table != nullptr || ptab != nullptr)
         hipLaunchKernelGGL(serial_walk_blocks_kernel, dim3((uint32_t)((nt + 255) / 256)), dim3(256), 0, stream,
-                           ctrl, table, M, bend, path, lo, L, K, R, depth, nserial);
+                           ctrl, table, M, bend, path, lo, L, K, R, depth, nserial, ptab,
+                           make_fastdiv(spp ? spp : 1u));
     hipLaunchKernelGGL(serial_walk_super_kernel, dim3((uint32_t)((nst + 255) / 256)), dim3(256), 0, stream,
                        ctrl, bend, lo, sbend, sB, L, K, R, nserial);
     hipLaunchKernelGGL(serial_walk_finish_kernel, dim3(1), dim3(256), 0, stream, ctrl, table, M, V, npix,

@@ -82,6 +82,7 @@ size_t tile_row(size_t k, uint32_t row_block, uint32_t rank, uint32_t nranks) {
 
 static_assert(kPrimaryTriStripW == kTriStripW, "render.h and bvh.h strip widths");
 static constexpr uint64_t kMaxParts = 1024;  // job-queue partitions (render.hip)
+static constexpr uint32_t kPixtabParts = 64;  // the pixel table pass's (zeroed by the window kernel)
 
 static int device_for(WorldState &w, int want, DeviceState *&out) {
     int count = 0;
@@ -621,7 +622,11 @@ int render_frame(WorldState &w, const CameraModel &cam, size_t width, size_t hei
             1, std::min<uint64_t>({(uint64_t)(p.step ? 64 : 16), kMaxParts, njobs / (16 * chunk) + 1}));
         if (const uint64_t np = env_u64("RT_AMD_SERIAL_PARTS", 0)) parts = std::min<uint64_t>(np, kMaxParts);
         p.nparts = (uint32_t)parts;
-        if (sp->mode == kRngSerialCoalesce) {
+        if (sp->mode == kRngSerialPixel) {
+            // (job counters zeroed by serial_window_kernel, kPixtabParts of them)
+            p.nparts = (uint32_t)std::min<uint64_t>(parts, kPixtabParts);
+            HIP_TRY(launch_trace(p, (uint32_t)blocks, s));
+        } else if (sp->mode == kRngSerialCoalesce) {
             // one workgroup per block of sp->R samples; the tree in LDS when it
             // fits beside the search's own arrays (64 KB per workgroup)
             const bool tree_lds = p.use_lds && serial_coalesce_lds(p, sp->variants, true) <= 64 * 1024;
@@ -954,9 +959,13 @@ static int serial_find_states(WorldState &w, const CameraModel &cam, size_t widt
         const uint64_t npq_max = L / spp + 2;
         const uint64_t emax = pixtab ? serial_pixtab_emax((uint32_t)spp, (uint32_t)K, depth) : 0;
         if (pixtab && (npq_max * emax > (1ull << 28) || emax > 0x7FFFFFFFull)) pixtab = false;
+        // the block walks read the pixel table directly (RT_AMD_SERIAL_PGATHER=1:
+        // through a gathered L x K count table instead, the first build: 27 us per
+        // iteration more at 32 k x 617)
+        const bool pgather = pixtab && env_u64("RT_AMD_SERIAL_PGATHER", 0) != 0;
         if (pixtab) {
             HIP_TRY(grow(d->sptab, d->sptab_cap, npq_max * emax));
-            HIP_TRY(grow(d->samples, d->samples_cap, L * K));
+            if (pgather) HIP_TRY(grow(d->samples, d->samples_cap, L * K));
         }
         // The walks size each iteration's windows from the per-pixel variances
         // (V: prefix sums over pixels of spp var, then var; the variance of
@@ -992,7 +1001,7 @@ static int serial_find_states(WorldState &w, const CameraModel &cam, size_t widt
         HIP_TRY(grow(d->ssbend, d->ssbend_cap, serial_super_words((uint32_t)L, (uint32_t)K, (uint32_t)R_walk)));
         // recorded block paths: the states of resolved samples become a gather
         // (the coalescing search has no count table to re-walk: always)
-        const bool gather = coalesce || env_u64("RT_AMD_SERIAL_GATHER", 1) != 0;
+        const bool gather = coalesce || pixtab || env_u64("RT_AMD_SERIAL_GATHER", 1) != 0;
         if (gather) {
             HIP_TRY(grow(d->spath, d->spath_cap, (L + R_walk - 1) / R_walk * R_walk * K));
             if (!d->sfin) HIP_TRY(hipMalloc((void **)&d->sfin, (4 + kMaxWalkBlocks) * 4));
@@ -1028,9 +1037,11 @@ static int serial_find_states(WorldState &w, const CameraModel &cam, size_t widt
             }
             const auto t0 = std::chrono::steady_clock::now();
             for (uint64_t q = 0; q < it; ++q) {
+                // (the pixel table pass's job counters are zeroed by the window kernel)
                 HIP_TRY(launch_serial_window(d->sctrl, d->sjump, d->swin, (uint32_t)wlen, pred, d->slo,
                                              (uint32_t)L, (uint32_t)K, depth, (uint32_t)N,
-                                             pixtab ? (uint32_t)spp : 0u, s));
+                                             pixtab ? (uint32_t)spp : 0u, pixtab ? d->counter : nullptr,
+                                             kPixtabParts, s));
                 if (pixtab) {
                     SerialPass sp{kRngSerialPixel, 0u, (uint32_t)npq_max, (uint32_t)emax, d->swin, pred, d->sctrl,
                                   d->slo};
@@ -1039,8 +1050,9 @@ static int serial_find_states(WorldState &w, const CameraModel &cam, size_t widt
                     sp.Kmax = (uint32_t)K;
                     rc = render_frame(w, cam, width, height, ob, nullptr, s, nullptr, &sp);
                     if (rc) return rc;
-                    HIP_TRY(launch_serial_pixtab_gather(d->sctrl, d->sptab, d->slo, d->samples, (uint32_t)L,
-                                                       (uint32_t)K, (uint32_t)spp, (uint32_t)N, s));
+                    if (pgather)
+                        HIP_TRY(launch_serial_pixtab_gather(d->sctrl, d->sptab, d->slo, d->samples, (uint32_t)L,
+                                                           (uint32_t)K, (uint32_t)spp, (uint32_t)N, s));
                 } else {
                     SerialPass sp{coalesce ? kRngSerialCoalesce : kRngSerialCount, 0u, (uint32_t)L, (uint32_t)K,
                                   d->swin, pred, d->sctrl, d->slo};
@@ -1051,12 +1063,13 @@ static int serial_find_states(WorldState &w, const CameraModel &cam, size_t widt
                     rc = render_frame(w, cam, width, height, ob, nullptr, s, nullptr, &sp);
                     if (rc) return rc;
                 }
-                HIP_TRY(launch_serial_walk(d->sctrl, coalesce ? nullptr : d->samples, pred, adapt ? Vdev : nullptr,
-                                           (uint32_t)npix, (uint32_t)spp, (float)z, (float)serial_floor(spp * R),
-                                           d->swin, d->sstates, d->sbend, gather ? d->spath : nullptr,
-                                           gather ? d->sfin : nullptr, d->slo, d->ssbend, d->ssb, (uint32_t)L,
-                                           (uint32_t)Lw, (uint32_t)K, (uint32_t)R_walk, depth,
-                                           (uint32_t)N, s));
+                HIP_TRY(launch_serial_walk(d->sctrl, (coalesce || (pixtab && !pgather)) ? nullptr : d->samples, pred,
+                                           adapt ? Vdev : nullptr, (uint32_t)npix, (uint32_t)spp, (float)z,
+                                           (float)serial_floor(spp * R), d->swin, d->sstates, d->sbend,
+                                           gather ? d->spath : nullptr, gather ? d->sfin : nullptr, d->slo,
+                                           d->ssbend, d->ssb, (uint32_t)L, (uint32_t)Lw, (uint32_t)K,
+                                           (uint32_t)R_walk, depth, (uint32_t)N,
+                                           (pixtab && !pgather) ? d->sptab : nullptr, s));
             }
             const auto t1 = std::chrono::steady_clock::now();
             HIP_TRY(hipMemcpyAsync(ctrl, d->sctrl, 32, hipMemcpyDeviceToHost, s));

@@ -108,6 +108,8 @@ def test_serial_narrow_windows_and_short_iterations(monkeypatch):
         (dict(RT_AMD_SERIAL_CHUNK="9"), "world.txt", (13, 7, 16, 8)),
         (dict(RT_AMD_SERIAL_CHUNK="50", RT_AMD_SERIAL_K="8"), "world.txt", (7, 5, 33, 4)),
         (dict(RT_AMD_SERIAL_PCHUNK="1000"), "world.txt", (33, 17, 5, 8)),
+        # pixel table through a gathered count table (the first build's walks)
+        (dict(RT_AMD_SERIAL_PGATHER="1", RT_AMD_SERIAL_K="40"), "c_raytracer_world.txt", (40, 30, 16, 8)),
     ]:
         for k, v in env.items():
             monkeypatch.setenv(k, v)
