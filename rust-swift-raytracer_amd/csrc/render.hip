@@ -821,6 +821,29 @@ void trace_kernel(TraceParams p) {
         }
     }
     const uint32_t lane = __lane_id();
+    // Each section of the loop (ray setup, sphere walk, triangle setup and
+    // walk, shading, the chunk resolve, the refill) re-reads the parameters it
+    // needs from the kernarg segment (scalar loads through a pointer the
+    // compiler must treat as changed each time) instead of holding all of
+    // them in SGPRs across the whole loop: the lean C2 kernel spilled 92 SGPRs
+    // to VGPR lanes (252 v_readlane / v_writelane in its code), the C5 kernel
+    // 191 plus 13 VGPRs to scratch; now 7 and 0 (+3 VGPRs).  A/B in one
+    // process (tools/ab.py, lean frames): C2 4.638 -> 4.451 ms, C3 69.61 ->
+    // 66.86 ms, C5 175.1 -> 170.9 ms (profiles/round4_kargs/).
+    // RT_NO_KARG_RELOAD builds the previous code.
+    // (SERIAL passes rewrite fields of their copy of p at entry -- cbase, spp,
+    // the divider, njobs -- so they keep reading that copy)
+    auto kargs = [&]() -> const TraceParams & {
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(RT_NO_KARG_RELOAD)
+        if (kSerial) return p;
+        const __attribute__((address_space(4))) TraceParams *kp =
+            (const __attribute__((address_space(4))) TraceParams *)__builtin_amdgcn_kernarg_segment_ptr();
+        asm volatile("" : "+s"(kp));
+        return *(const TraceParams *)kp;
+#else
+        return p;
+#endif
+    };
     extern __shared__ float4 lds[];
     BvhView view;
     const uint32_t sph_root = stage_tree<kLds>(p, lds, view);  // the sphere walk's first node
@@ -922,6 +945,7 @@ void trace_kernel(TraceParams p) {
             // search ends early are shaded and refilled while the others walk on.
             float out_r = 0.0f, out_g = 0.0f, out_b = 0.0f;
             if (phase == kSetup) {
+                const TraceParams &p = kargs();  // (ray setup: see kargs)
                 if ((int32_t)bounce >= p.depth) {
                     done = true;  // depth exhausted -> (0, 0, 0) (common.rs:284)
                 } else {
@@ -978,6 +1002,7 @@ void trace_kernel(TraceParams p) {
                 walk_now = nwalk >= p.walk_min || nother == 0;
             }
             if (kBvh && phase == kSph && walk_now) {
+                const TraceParams &p = kargs();  // (see kargs)
                 walked = true;
                 constexpr uint32_t kEnd = kLds ? 0xFFFFu : kNodeEndDev;
                 const SphBound bnd = sph_bound(p, org);
@@ -995,6 +1020,7 @@ void trace_kernel(TraceParams p) {
                 if (node == kEnd) phase = kTriInit;
             }
             if (phase == kTriInit) {
+                const TraceParams &p = kargs();  // (see kargs)
                 // Mesh::hit with t_max = best_t, own closest from +inf (common.rs:178-223)
                 tri_t = __builtin_inff();
                 tri_i = -1;
@@ -1025,6 +1051,7 @@ void trace_kernel(TraceParams p) {
                 tri_now = nwalk >= p.tri_walk_min || nother == 0;
             }
             if (kMesh == 2 && phase == kTri && tri_now) {
+                const TraceParams &p = kargs();  // (see kargs)
                 if (kStep) budget = max(budget, p.steps / 2u);  // a lane that just left the sphere walk
                 const bool cam = bounce == 0 && p.cam_nnodes != 0;
                 const F3 dlt2 = f3(2.0f * (org.x - p.tbvh_oc[0]), 2.0f * (org.y - p.tbvh_oc[1]),
@@ -1044,6 +1071,7 @@ void trace_kernel(TraceParams p) {
             }
             RT_STAMP(2);
             if (phase == kShade) {
+                const TraceParams &p = kargs();  // (see kargs)
                 phase = kSetup;
                 if (tri_i < 0 && best_i < 0) {
                     // background (common.rs:276-281): re-normalise, lerp to sky blue
@@ -1173,8 +1201,9 @@ void trace_kernel(TraceParams p) {
                     const uint32_t n = (uint32_t)__popcll(__ballot(fin && lk == k));
                     rleft[k] -= n;
                     if (n != 0 && rleft[k] == 0) {
-                        if (!(p.ablate & 2u))
-                            resolve_chunk<kMesh != 2>(p, sbase, pstride, k << p.ring_shift, rbase[k],
+                        const TraceParams &pc = kargs();
+                        if (!(pc.ablate & 2u))
+                            resolve_chunk<kMesh != 2>(pc, sbase, pstride, k << pc.ring_shift, rbase[k],
                                                   rlen[k], lane);
                         rfree |= 1u << k;
                     }
@@ -1186,16 +1215,17 @@ void trace_kernel(TraceParams p) {
         // (with the fused resolve a new chunk needs a free ring slot: with all
         // kTraceRing slots waiting on unfinished samples the lanes stay idle)
         if (refill && !exhausted && !(fused && rfree == 0 && pool_next >= pool_end)) {
+            const TraceParams &pc = kargs();  // (the refill's parameters: see kargs)
             if (pool_next >= pool_end) {
                 uint32_t base = 0;
                 if (lane == 0) {
                     base = pbegin + (prefetch_pending ? prefetch
-                                                      : atomicAdd(p.job_counter + 32u * part, p.chunk));
-                    while (base >= pend && ++tries < p.nparts) {
-                        part = part + 1 == p.nparts ? 0 : part + 1;
+                                                      : atomicAdd(pc.job_counter + 32u * part, pc.chunk));
+                    while (base >= pend && ++tries < pc.nparts) {
+                        part = part + 1 == pc.nparts ? 0 : part + 1;
                         pbegin = part_begin(part);
                         pend = part_begin(part + 1);
-                        base = pbegin + atomicAdd(p.job_counter + 32u * part, p.chunk);
+                        base = pbegin + atomicAdd(pc.job_counter + 32u * part, pc.chunk);
                     }
                 }
                 prefetch_pending = false;
@@ -1211,7 +1241,7 @@ void trace_kernel(TraceParams p) {
 #endif
                 } else {
                     pool_next = base;
-                    pool_end = min(base + p.chunk, pend);
+                    pool_end = min(base + pc.chunk, pend);
 #ifdef RT_WAVE_TIMES
                     wt_pull = __builtin_amdgcn_s_memrealtime();
                     wt_jobs_tail = pool_end - pool_next;
@@ -1222,7 +1252,7 @@ void trace_kernel(TraceParams p) {
 #pragma unroll
                         for (uint32_t i = 0; i < kTraceRing; ++i)
                             if (i == k) rbase[i] = base, rlen[i] = rleft[i] = pool_end - base;
-                        cur_off = (k << p.ring_shift) - base;
+                        cur_off = (k << pc.ring_shift) - base;
                     }
                 }
             }
@@ -1239,16 +1269,16 @@ void trace_kernel(TraceParams p) {
                 // states use the reference's job index below, so the
                 // enumeration order changes no bits.
                 uint32_t s, col, row;
-                job_pixel<kSerial>(p, job, s, col, row);
+                job_pixel<kSerial>(pc, job, s, col, row);
                 slot = job + cur_off;
                 bool take = true;
                 if (kSerial) {
                     nscat = 0;
-                    rng = serial_start(p, job);
-                    if (p.mode == kRngSerialPixel) take = serial_pixel_job(p, job);
+                    rng = serial_start(pc, job);
+                    if (pc.mode == kRngSerialPixel) take = serial_pixel_job(pc, job);
                 } else {
-                    const uint64_t gjob = ((uint64_t)row * p.width + col) * p.spp + s;
-                    rng = (p.mode == kRngReplay) ? p.replay[gjob] : counter_seed(p.seed, gjob);
+                    const uint64_t gjob = ((uint64_t)row * pc.width + col) * pc.spp + s;
+                    rng = (pc.mode == kRngReplay) ? pc.replay[gjob] : counter_seed(pc.seed, gjob);
                 }
                 // common.rs:335-337: u drawn before v; camera.rs:84-89
                 // numerators are in [2^-32, 2^24]: exactdiv.h with the host's
@@ -1256,26 +1286,26 @@ void trace_kernel(TraceParams p) {
                 const float un = (float)col + draw01(rng);
                 const float vn = (float)row + draw01(rng);
 #ifndef RT_NO_XDIV
-                const bool xd = p.xdiv_uv != 0;
+                const bool xd = pc.xdiv_uv != 0;
 #else
                 const bool xd = false;
 #endif
-                const float u = xd ? xdiv(un, p.wden, p.wrcp) : un / p.wden;
-                const float v = xd ? xdiv(vn, p.hden, p.hrcp) : vn / p.hden;
-                const F3 h = f3(p.cam[6], p.cam[7], p.cam[8]);
-                const F3 vv = f3(p.cam[9], p.cam[10], p.cam[11]);
-                org = f3(p.cam[0], p.cam[1], p.cam[2]);
-                const F3 llc = f3(p.cam[3], p.cam[4], p.cam[5]);
+                const float u = xd ? xdiv(un, pc.wden, pc.wrcp) : un / pc.wden;
+                const float v = xd ? xdiv(vn, pc.hden, pc.hrcp) : vn / pc.hden;
+                const F3 h = f3(pc.cam[6], pc.cam[7], pc.cam[8]);
+                const F3 vv = f3(pc.cam[9], pc.cam[10], pc.cam[11]);
+                org = f3(pc.cam[0], pc.cam[1], pc.cam[2]);
+                const F3 llc = f3(pc.cam[3], pc.cam[4], pc.cam[5]);
                 vdir = ((llc + scale(h, u)) + scale(vv, v)) - org;  // normalised below
                 renorm = true;
-                if (kBvh && !kMesh && p.spl != nullptr) {
+                if (kBvh && !kMesh && pc.spl != nullptr) {
                     // issued after the seed's (replay) load, so nothing waits on it
                     // before the ray's setup in the next iteration
-                    if (p.ablate & 4u) {  // timing-only diagnostic: no record load
+                    if (pc.ablate & 4u) {  // timing-only diagnostic: no record load
                         spl0 = 0;
                         spl1 = 0;
                     } else {
-                        const uint2 r = p.spl[(size_t)(p.height - 1u - row) * p.width + col];
+                        const uint2 r = pc.spl[(size_t)(pc.height - 1u - row) * pc.width + col];
                         spl0 = r.x;
                         spl1 = r.y;
                     }
