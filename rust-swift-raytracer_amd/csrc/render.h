@@ -278,14 +278,15 @@ hipError_t launch_assemble(const uint32_t *gathered, uint32_t *out, uint32_t wid
                            hipStream_t stream);
 // variant: 0 brute force, 1 BVH from global memory, 2 BVH staged in LDS;
 // step: the sliced-walk kernel (TraceParams::step); mesh: trace_mesh_kind
-// workgroups per CU of one trace_kernel instance (count: the counting variant)
+// workgroups per CU of one trace_kernel instance (kind: 0 the lean frame
+// kernel, 1 the counting frame kernel, 2 the SERIAL passes)
 hipError_t trace_occupancy(int *blocks_per_cu, int variant, size_t lds_bytes, bool step, int mesh,
-                           bool count);
+                           int kind);
 // The kernel family of a scene: 0 no triangles, 1 triangles searched by brute
 // force (no triangle tree), 2 triangle trees (TraceParams::tnodes != 0)
 inline int trace_mesh_kind(bool triangles, bool tree) { return !triangles ? 0 : tree ? 2 : 1; }
 size_t trace_lds_bytes(const TraceParams &p);
 // threads per trace workgroup: LDS-tree kernels (sphere-only scenes or not) vs global
-uint32_t trace_block_threads(bool lds, bool mesh);
+uint32_t trace_block_threads(bool lds, bool mesh, int kind);
 
 }  // namespace rtamd

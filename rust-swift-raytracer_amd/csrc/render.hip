@@ -770,14 +770,30 @@ __device__ __forceinline__ uint32_t stage_tree(const TraceParams &p, float4 *lds
 #ifndef RT_WAVES_PER_EU_MESH
 #define RT_WAVES_PER_EU_MESH 6
 #endif
-// LDS workgroup of the sphere-only kernel: 768 threads, 2 per CU (6 waves
-// per SIMD).  Measured on C2 (A/B, one process): 512 -> 6.77 ms, 768 -> 6.73,
-// 896 -> 8.41, 1024 (8 waves/SIMD) -> 7.78 (above 6 waves per SIMD the
-// per-wave ray state thrashes the L1); with the current kernel 256 -> 7.90,
-// 384 -> 6.15, 512 -> 5.42 = 768 at N = 1, and on the 8-rank tile 768 beats
-// 512 by 3 % (0.90 vs 0.93 ms).
+// LDS workgroup of the sphere-only kernel: 1024 threads, 2 per CU (8 waves
+// per SIMD, RT_WAVES_PER_EU_SPHERES).  History (A/B, one process): round 1,
+// 512 -> 6.77 ms, 768 -> 6.73, 896 -> 8.41, 1024 -> 7.78 (then the per-wave ray
+// state thrashed the L1); round 2, 256 -> 7.90, 384 -> 6.15, 512 -> 5.42 = 768,
+// and on the 8-rank tile 768 beat 512 by 3 %.  Round 4, after the kernarg
+// reloads freed the SGPRs (profiles/round4_occ/ab_occ_*.log, rank_occ_*.log):
+// 768 -> 1024 at 8 waves: C2 4.449 -> 4.444 ms, C3 66.86 -> 62.23 ms, C2 tiles
+// of 2 / 8 ranks 2.389 -> 2.336 / 0.772 -> 0.781 ms, C3 8-rank tile 8.78 ->
+// 8.33 ms; 896 (7 waves) -> one workgroup per CU, 6.0 ms.  The counting and
+// SERIAL sphere variants keep 768 threads at RT_WAVES_PER_EU: at 8 waves their
+// extra state spills VGPRs to scratch.
+#ifndef RT_WAVES_PER_EU_SPHERES
+#define RT_WAVES_PER_EU_SPHERES 8
+#endif
 #ifndef RT_LDS_BLOCK_SPHERES
-#define RT_LDS_BLOCK_SPHERES 768
+#define RT_LDS_BLOCK_SPHERES 1024
+#endif
+// (the sphere kernels without the LDS tree, 256 threads: A/B 8 vs 6 waves,
+// global-memory tree at C2 6.01 vs 5.99 ms, brute force 2.39 vs 2.32 ms)
+#ifndef RT_WAVES_PER_EU_SPHERES_GLOBAL
+#define RT_WAVES_PER_EU_SPHERES_GLOBAL 6
+#endif
+#ifndef RT_LDS_BLOCK_SPHERES_AUX
+#define RT_LDS_BLOCK_SPHERES_AUX 768
 #endif
 // LDS workgroup of the triangle-scene kernels (A/B on C5: 256 -> 223 ms,
 // 512 -> 221, 768 -> 225)
@@ -789,9 +805,18 @@ __device__ __forceinline__ uint32_t stage_tree(const TraceParams &p, float4 *lds
 // kSerial: the SERIAL-mode passes (render.h kRngSerial*): jobs are (sample,
 // variant) pairs and store scatter counts -- a separate instance, so the frame
 // kernels carry none of its registers.
+// kind: 0 lean frame kernel, 1 counting frame kernel, 2 SERIAL pass
+constexpr uint32_t trace_threads(bool lds, bool mesh, int kind) {
+    return !lds ? 256u : mesh ? (uint32_t)RT_LDS_BLOCK_MESH
+                       : kind == 0 ? (uint32_t)RT_LDS_BLOCK_SPHERES : (uint32_t)RT_LDS_BLOCK_SPHERES_AUX;
+}
+constexpr int trace_waves_per_eu(bool lds, bool mesh, int kind) {
+    return kind != 0 ? RT_WAVES_PER_EU : mesh ? RT_WAVES_PER_EU_MESH
+                       : lds ? RT_WAVES_PER_EU_SPHERES : RT_WAVES_PER_EU_SPHERES_GLOBAL;
+}
 template <bool kBvh, bool kLds, bool kStep, int kMesh, bool kCount, bool kSerial = false>
-__global__ __launch_bounds__(kLds ? (kMesh != 0 ? RT_LDS_BLOCK_MESH : RT_LDS_BLOCK_SPHERES) : 256)
-__attribute__((amdgpu_waves_per_eu((kMesh != 0 && !kCount) ? RT_WAVES_PER_EU_MESH : RT_WAVES_PER_EU, 8)))
+__global__ __launch_bounds__(trace_threads(kLds, kMesh != 0, kSerial ? 2 : kCount ? 1 : 0))
+__attribute__((amdgpu_waves_per_eu(trace_waves_per_eu(kLds, kMesh != 0, kSerial ? 2 : kCount ? 1 : 0), 8)))
 void trace_kernel(TraceParams p) {
     // SERIAL count passes: the walk of the previous pass set the first sample
     // and this iteration's candidates per sample (ctrl[5], <= the launch's K)
@@ -1423,9 +1448,7 @@ __global__ __launch_bounds__(kResolveWaves * 64) void resolve_kernel(
 
 }  // namespace
 
-uint32_t trace_block_threads(bool lds, bool mesh) {
-    return lds ? (mesh ? (uint32_t)RT_LDS_BLOCK_MESH : (uint32_t)RT_LDS_BLOCK_SPHERES) : 256u;
-}
+uint32_t trace_block_threads(bool lds, bool mesh, int kind) { return trace_threads(lds, mesh, kind); }
 
 size_t trace_lds_bytes(const TraceParams &p) {
     // (shading records in global memory instead, which would allow 8 waves per
@@ -1437,7 +1460,7 @@ template <bool kStep, int kMesh, bool kCount, bool kSerial>
 static void launch_trace_t(const TraceParams &p, uint32_t blocks, hipStream_t stream) {
     if (p.nnodes && p.use_lds)
         hipLaunchKernelGGL((trace_kernel<true, true, kStep, kMesh, kCount, kSerial>), dim3(blocks),
-                           dim3(trace_block_threads(true, kMesh != 0)),
+                           dim3(trace_threads(true, kMesh != 0, kSerial ? 2 : kCount ? 1 : 0)),
                            trace_lds_bytes(p), stream, p);
     else if (p.nnodes)
         hipLaunchKernelGGL((trace_kernel<true, false, kStep, kMesh, kCount, kSerial>), dim3(blocks),
@@ -1482,35 +1505,37 @@ hipError_t launch_resolve_ex(const float *samples, uint32_t *out, uint32_t npix,
     return hipGetLastError();
 }
 
-template <bool kStep, int kMesh, bool kCount>
+template <bool kStep, int kMesh, bool kCount, bool kSerial>
 static hipError_t trace_occupancy_t(int *blocks_per_cu, int variant, size_t lds_bytes) {
+    constexpr int kind = kSerial ? 2 : kCount ? 1 : 0;
     if (variant == 2)
         return hipOccupancyMaxActiveBlocksPerMultiprocessor(
-            blocks_per_cu, trace_kernel<true, true, kStep, kMesh, kCount>,
-            trace_block_threads(true, kMesh != 0), lds_bytes);
+            blocks_per_cu, trace_kernel<true, true, kStep, kMesh, kCount, kSerial>,
+            trace_threads(true, kMesh != 0, kind), lds_bytes);
     if (variant == 1)
         return hipOccupancyMaxActiveBlocksPerMultiprocessor(
-            blocks_per_cu, trace_kernel<true, false, kStep, kMesh, kCount>, 256, 0);
+            blocks_per_cu, trace_kernel<true, false, kStep, kMesh, kCount, kSerial>, 256, 0);
     return hipOccupancyMaxActiveBlocksPerMultiprocessor(
-        blocks_per_cu, trace_kernel<false, false, kStep, kMesh, kCount>, 256, 0);
+        blocks_per_cu, trace_kernel<false, false, kStep, kMesh, kCount, kSerial>, 256, 0);
 }
 
-template <bool kCount>
+template <bool kCount, bool kSerial>
 static hipError_t trace_occupancy_c(int *blocks_per_cu, int variant, size_t lds_bytes, bool step,
                                     int mesh) {
     if (step)
-        return mesh == 2   ? trace_occupancy_t<true, 2, kCount>(blocks_per_cu, variant, lds_bytes)
-               : mesh == 1 ? trace_occupancy_t<true, 1, kCount>(blocks_per_cu, variant, lds_bytes)
-                           : trace_occupancy_t<true, 0, kCount>(blocks_per_cu, variant, lds_bytes);
-    return mesh == 2   ? trace_occupancy_t<false, 2, kCount>(blocks_per_cu, variant, lds_bytes)
-           : mesh == 1 ? trace_occupancy_t<false, 1, kCount>(blocks_per_cu, variant, lds_bytes)
-                       : trace_occupancy_t<false, 0, kCount>(blocks_per_cu, variant, lds_bytes);
+        return mesh == 2   ? trace_occupancy_t<true, 2, kCount, kSerial>(blocks_per_cu, variant, lds_bytes)
+               : mesh == 1 ? trace_occupancy_t<true, 1, kCount, kSerial>(blocks_per_cu, variant, lds_bytes)
+                           : trace_occupancy_t<true, 0, kCount, kSerial>(blocks_per_cu, variant, lds_bytes);
+    return mesh == 2   ? trace_occupancy_t<false, 2, kCount, kSerial>(blocks_per_cu, variant, lds_bytes)
+           : mesh == 1 ? trace_occupancy_t<false, 1, kCount, kSerial>(blocks_per_cu, variant, lds_bytes)
+                       : trace_occupancy_t<false, 0, kCount, kSerial>(blocks_per_cu, variant, lds_bytes);
 }
 
 hipError_t trace_occupancy(int *blocks_per_cu, int variant, size_t lds_bytes, bool step, int mesh,
-                           bool count) {
-    return count ? trace_occupancy_c<true>(blocks_per_cu, variant, lds_bytes, step, mesh)
-                 : trace_occupancy_c<false>(blocks_per_cu, variant, lds_bytes, step, mesh);
+                           int kind) {
+    return kind == 2   ? trace_occupancy_c<false, true>(blocks_per_cu, variant, lds_bytes, step, mesh)
+           : kind == 1 ? trace_occupancy_c<true, false>(blocks_per_cu, variant, lds_bytes, step, mesh)
+                       : trace_occupancy_c<false, false>(blocks_per_cu, variant, lds_bytes, step, mesh);
 }
 
 // ------------------------------------------------------------ SERIAL mode

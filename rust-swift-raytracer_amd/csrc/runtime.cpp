@@ -111,7 +111,7 @@ static int device_for(WorldState &w, int want, DeviceState *&out) {
         // the scene's kernel family (render.h trace_mesh_kind; frames rendered with
         // RT_ACCEL_BRUTE run the brute-force triangle kernels on these figures)
         const int tri = trace_mesh_kind(w.packed.ntri > 0, !w.tbvh.nodes.empty());
-        for (int c = 0; c < 2; ++c)
+        for (int c = 0; c < 3; ++c)
             for (int st = 0; st < 2; ++st) {
                 HIP_TRY(trace_occupancy(&d->blocks_per_cu[c][st], 0, 0, st, tri, c));
                 HIP_TRY(trace_occupancy(&d->blocks_per_cu_bvh[c][st], 1, 0, st, tri, c));
@@ -166,7 +166,7 @@ static int device_for(WorldState &w, int want, DeviceState *&out) {
                 HIP_TRY(hipMalloc((void **)&d->bvh_miss16, m16.size() * 2));
                 HIP_TRY(hipMemcpy(d->bvh_miss16, m16.data(), m16.size() * 2, hipMemcpyHostToDevice));
                 bool fits = true;
-                for (int c = 0; c < 2; ++c)
+                for (int c = 0; c < 3; ++c)
                     for (int st = 0; st < 2; ++st) {
                         HIP_TRY(trace_occupancy(&d->blocks_per_cu_lds[c][st], 2, lds, st, tri, c));
                         fits = fits && d->blocks_per_cu_lds[c][st] > 0;
@@ -189,7 +189,7 @@ static int device_for(WorldState &w, int want, DeviceState *&out) {
             d->tloose = (uint32_t)tb.loose.size();
         }
         const uint64_t bpc = env_u64("RT_AMD_BLOCKS_PER_CU", 0);
-        for (int c = 0; c < 2; ++c)
+        for (int c = 0; c < 3; ++c)
             for (int st = 0; st < 2; ++st) {
                 if (bpc)
                     d->blocks_per_cu[c][st] = d->blocks_per_cu_bvh[c][st] = d->blocks_per_cu_lds[c][st] =
@@ -559,11 +559,12 @@ int render_frame(WorldState &w, const CameraModel &cam, size_t width, size_t hei
     p.tri_walk_min = (uint32_t)env_u64("RT_AMD_TRI_WALK_MIN", 32);
     const int sv = p.step ? 1 : 0;
     const bool timed = stats != nullptr;  // HIP-event timing + counters need a host wait
-    const int ctv = timed ? 1 : 0;         // launch_trace runs the counting variant iff p.stats
+    // launch_trace runs the counting variant iff p.stats, the SERIAL instances for sp
+    const int ctv = sp ? 2 : timed ? 1 : 0;
     const int bpc = !use_bvh   ? d->blocks_per_cu[ctv][sv]
                     : p.use_lds ? d->blocks_per_cu_lds[ctv][sv]
                                 : d->blocks_per_cu_bvh[ctv][sv];
-    const uint64_t waves_per_block = trace_block_threads(use_bvh && p.use_lds, p.ntri != 0) / 64;
+    const uint64_t waves_per_block = trace_block_threads(use_bvh && p.use_lds, p.ntri != 0, ctv) / 64;
     const uint64_t full_blocks = (uint64_t)bpc * (uint64_t)d->num_cus;
     double trace_ms = 0.0, resolve_ms = 0.0;
     uint32_t launches = 0, waves = 0;

@@ -87,7 +87,7 @@ struct DeviceState {
     unsigned long long *stats = nullptr; size_t stats_cap = 0;  // per-wave counter records
     // resident workgroups per CU of each kernel variant, [0]: whole walks, [1]: sliced walks
     // [count][step]: workgroups per CU of each kernel instance
-    int blocks_per_cu[2][2] = {}, blocks_per_cu_bvh[2][2] = {}, blocks_per_cu_lds[2][2] = {};
+    int blocks_per_cu[3][2] = {}, blocks_per_cu_bvh[3][2] = {}, blocks_per_cu_lds[3][2] = {};
     int num_cus = 0;
     size_t last_jobs = 0;                                       // jobs of the last launch
     size_t last_spp = 0;                                        // and its spp
