@@ -489,7 +489,64 @@ TriangleBVH build_triangle_bvh(const std::vector<Triangle> &tris, const std::vec
     for (uint32_t oct = 0; oct < 8; ++oct) b.links(0, kNodeEnd, oct, out.miss);
     out.tris = triangle_records(prims, tris, tri_hot);
     quantize_boxes(out.nodes, 16, true, out.miss, out.qnodes, out.qbox, &out.nbase, &out.nstep);
+    build_wide_image(out);
     return out;
+}
+
+void build_wide_image(TriangleBVH &tb) {
+    tb.wnodes.clear();
+    tb.wdepth = 0;
+    const size_t n = tb.qnodes.size() / 8;
+    if (n == 0) return;
+    auto word = [&](uint32_t node, int k) { return tb.qnodes[(size_t)node * 8 + k]; };
+    auto is_leaf = [&](uint32_t node) { return (word(node, 6) & kLeafBit) != 0; };
+    auto child = [&](uint32_t node) { return word(node, 6) & 0x1FFFFFFFu; };
+    // the binary nodes a wide node holds: grandchildren of binary node b
+    auto slots = [&](uint32_t b, uint32_t out[4]) -> int {
+        int m = 0;
+        if (is_leaf(b)) {  // (a one-leaf tree: the root record holds node 0 itself)
+            out[m++] = b;
+            return m;
+        }
+        for (uint32_t c = child(b); c < child(b) + 2; ++c) {
+            if (is_leaf(c)) {
+                out[m++] = c;
+            } else {
+                out[m++] = child(c);
+                out[m++] = child(c) + 1;
+            }
+        }
+        return m;
+    };
+    // breadth-first: wide node w stands for binary node order[w]
+    std::vector<uint32_t> order{0}, depth{0};
+    for (size_t w = 0; w < order.size(); ++w) {
+        if (order.size() > 65535) return;  // u16 stack entries
+        uint32_t s[4];
+        const int m = slots(order[w], s);
+        for (int c = 0; c < m; ++c)
+            if (!is_leaf(s[c]) && !(order[w] == 0 && is_leaf(0))) {
+                order.push_back(s[c]);
+                depth.push_back(depth[w] + 1);
+            }
+    }
+    if (order.size() > 65535) return;
+    tb.wnodes.assign(order.size() * 32, 0u);
+    uint32_t next = 1;  // wide index of the next internal child, in the push order above
+    for (size_t w = 0; w < order.size(); ++w) {
+        uint32_t *r = &tb.wnodes[w * 32];
+        uint32_t s[4];
+        const int m = slots(order[w], s);
+        for (int c = 0; c < 4; ++c) {
+            if (c >= m) {
+                r[24 + c] = kLeafBit;  // empty: a leaf without triangles
+                continue;
+            }
+            for (int k = 0; k < 6; ++k) r[6 * c + k] = word(s[c], k);
+            r[24 + c] = is_leaf(s[c]) ? word(s[c], 6) : next++;
+        }
+        tb.wdepth = std::max(tb.wdepth, depth[w]);
+    }
 }
 
 CameraTriangleBVH build_camera_triangle_bvh(const std::vector<Triangle> &tris,

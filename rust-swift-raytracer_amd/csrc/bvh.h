@@ -75,7 +75,19 @@ struct TriangleBVH {
     std::vector<uint32_t> qnodes;
     QuantGrid qbox;
     float nbase = -1, nstep = 1;    // normal grid (all three axes)
+    // 4-wide image of the same tree (render.hip tri_wide): one 128-B record per
+    // wide node, 32 u32: child c's box and normal-box words (qnodes words 0-5 of
+    // the binary node it is) at 6c..6c+5, child words at 24..27 -- internal:
+    // the child's wide index; leaf: the qnode leaf word (kLeafBit | first << 3 |
+    // count); empty slot: kLeafBit (no triangles) -- and 28..31 zero.  Wide
+    // node = a binary node's grandchildren (a leaf child stays itself); the
+    // root record holds binary node 0's.  Breadth-first, root 0.  Empty when
+    // there are more than 65535 wide nodes (the walk's stack holds u16).
+    std::vector<uint32_t> wnodes;
+    uint32_t wdepth = 0;            // deepest wide node fetched (root 0): stack <= 3 * wdepth
 };
+// Fills tb.wnodes / tb.wdepth from tb.qnodes (build_triangle_bvh calls it).
+void build_wide_image(TriangleBVH &tb);
 
 // tri_hot: PackedScene::tri_hot (the exact per-triangle n and n.v0 bits).
 // oc (optional): origin the boxes are built for; phantom: SAH weight of the

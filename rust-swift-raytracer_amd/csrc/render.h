@@ -118,6 +118,12 @@ struct TraceParams {
     float tbvh_c[3], tbvh_r, tbvh_mag;
     float tbvh_oc[3];         // origin the boxes were built for (widening uses o - oc)
     float tq_base[3], tq_step[3], tq_nbase, tq_nstep;  // static-tree grids
+    // the static tree's 4-wide image (bvh.h TriangleBVH::wnodes), walked with a
+    // per-lane stack of tw_depth u16 entries in LDS (trace_kernel<..., kMesh = 3>);
+    // nullptr: the binary walk (kMesh = 2)
+    const uint4 *tw_nodes;    // 8 per wide node (128 B)
+    uint32_t tw_depth;        // stack entries per lane (3 * TriangleBVH::wdepth, >= 1)
+    uint32_t wsteps;          // wide-node fetches per lane per loop iteration (sliced walks)
     float cq_base[3], cq_step[3];                      // camera-tree grid
     // the same triangles' phantoms for the camera origin (bvh.h CameraTriangleBVH),
     // used at bounce 0; cam_nnodes == 0: bounce 0 uses the tree above
@@ -285,8 +291,18 @@ hipError_t trace_occupancy(int *blocks_per_cu, int variant, size_t lds_bytes, bo
 // The kernel family of a scene: 0 no triangles, 1 triangles searched by brute
 // force (no triangle tree), 2 triangle trees (TraceParams::tnodes != 0)
 inline int trace_mesh_kind(bool triangles, bool tree) { return !triangles ? 0 : tree ? 2 : 1; }
+// kMesh 3: kind 2 walked through the 4-wide image (TraceParams::tw_nodes); the
+// SERIAL passes keep the binary walk
 size_t trace_lds_bytes(const TraceParams &p);
-// threads per trace workgroup: LDS-tree kernels (sphere-only scenes or not) vs global
-uint32_t trace_block_threads(bool lds, bool mesh, int kind);
+// the sphere tree's LDS copy (render.hip stage_tree)
+__host__ __device__ inline size_t trace_tree_lds(uint32_t nnodes, uint32_t nprims, uint32_t nsph_padded) {
+    return (size_t)nnodes * 48 + (size_t)nprims * 20 + (size_t)nsph_padded * 36;
+}
+// threads per trace workgroup: LDS-tree kernels (per kernel family, trace_mesh_kind
+// or 3 for the wide walk) vs global
+uint32_t trace_block_threads(bool lds, int mesh, int kind);
+// dynamic LDS of one trace workgroup: the sphere tree (lds) and, for the wide
+// triangle walk, every lane's stack (u16 entries)
+size_t trace_dyn_lds(const TraceParams &p, bool lds, bool wide, uint32_t threads);
 
 }  // namespace rtamd

@@ -515,6 +515,47 @@ __device__ __forceinline__ bool tri_node(const TraceParams &p, F3 nlo, F3 nhi, F
     return !skip && is_leaf;
 }
 
+// One child of a 4-wide static-tree node (bvh.h TriangleBVH::wnodes): the
+// same decode, widening and skip rule as tri_node's static branch, from the
+// child's six box / normal-box words.  Returns whether the child is entered
+// (its entry distance in tn).
+__device__ __forceinline__ bool tri_wide_child(const TraceParams &p, uint32_t w0, uint32_t w1, uint32_t w2,
+                                               uint32_t w3, uint32_t w4, uint32_t w5, F3 nlo, F3 nhi,
+                                               F3 inv, F3 dlt2, float cap, float &tn) {
+    auto lo16 = [](uint32_t w) { return (float)(w & 0xFFFFu); };
+    auto hi16 = [](uint32_t w) { return (float)(w >> 16); };
+    const float gbx = p.tq_base[0], gsx = p.tq_step[0];
+    const float gby = p.tq_base[1], gsy = p.tq_step[1];
+    const float gbz = p.tq_base[2], gsz = p.tq_step[2];
+    const float nb = p.tq_nbase, ns = p.tq_nstep;
+    const float bx0 = __builtin_fmaf(lo16(w0), gsx, gbx), by0 = __builtin_fmaf(hi16(w0), gsy, gby);
+    const float bz0 = __builtin_fmaf(lo16(w1), gsz, gbz), bx1 = __builtin_fmaf(hi16(w1), gsx, gbx);
+    const float by1 = __builtin_fmaf(lo16(w2), gsy, gby), bz1 = __builtin_fmaf(hi16(w2), gsz, gbz);
+    const float nx0 = __builtin_fmaf(lo16(w3), ns, nb), ny0 = __builtin_fmaf(hi16(w3), ns, nb);
+    const float nz0 = __builtin_fmaf(lo16(w4), ns, nb), nx1 = __builtin_fmaf(hi16(w4), ns, nb);
+    const float ny1 = __builtin_fmaf(lo16(w5), ns, nb), nz1 = __builtin_fmaf(hi16(w5), ns, nb);
+    const float ax = nx0 * dlt2.x, bx = nx1 * dlt2.x;
+    const float ay = ny0 * dlt2.y, by = ny1 * dlt2.y;
+    const float az = nz0 * dlt2.z, bz = nz1 * dlt2.z;
+    const float sl = (fminf(ax, bx) + fminf(ay, by)) + fminf(az, bz);
+    const float sh = (fmaxf(ax, bx) + fmaxf(ay, by)) + fmaxf(az, bz);
+    auto widen = [&](float lo, float hi, float m0, float m1, float nl, float nh, float iv, float &t0,
+                     float &t1) {
+        const float a = sl * m0, b = sl * m1, c = sh * m0, d = sh * m1;
+        const float omin = fminf(fminf(a, b), fminf(c, d));
+        const float omax = fmaxf(fmaxf(a, b), fmaxf(c, d));
+        t0 = __builtin_fmaf(lo + omin, iv, nl);
+        t1 = __builtin_fmaf(hi + omax, iv, nh);
+    };
+    float t0x, t1x, t0y, t1y, t0z, t1z;
+    widen(bx0, bx1, nx0, nx1, nlo.x, nhi.x, inv.x, t0x, t1x);
+    widen(by0, by1, ny0, ny1, nlo.y, nhi.y, inv.y, t0y, t1y);
+    widen(bz0, bz1, nz0, nz1, nlo.z, nhi.z, inv.z, t0z, t1z);
+    tn = fmaxf(fmaxf(fminf(t0x, t1x), fminf(t0y, t1y)), fminf(t0z, t1z));
+    const float tf = fminf(fminf(fmaxf(t0x, t1x), fmaxf(t0y, t1y)), fmaxf(t0z, t1z));
+    return !(tn > tf || tf < 0.001f || __float_as_int(tn) > __float_as_int(cap));
+}
+
 __device__ __forceinline__ void tri_leaf(const TraceParams &p, F3 org, F3 dir, bool cam,
                                          uint32_t leaf, float best_t, float &tri_t, int &tri_i,
                                          uint32_t &tri_in, uint32_t &tri_done) {
@@ -806,17 +847,24 @@ __device__ __forceinline__ uint32_t stage_tree(const TraceParams &p, float4 *lds
 // variant) pairs and store scatter counts -- a separate instance, so the frame
 // kernels carry none of its registers.
 // kind: 0 lean frame kernel, 1 counting frame kernel, 2 SERIAL pass
-constexpr uint32_t trace_threads(bool lds, bool mesh, int kind) {
-    return !lds ? 256u : mesh ? (uint32_t)RT_LDS_BLOCK_MESH
+// Waves per SIMD of the wide triangle walk (kMesh 3; 80 VGPRs at 6)
+#ifndef RT_WAVES_PER_EU_WIDE
+#define RT_WAVES_PER_EU_WIDE 6
+#endif
+#ifndef RT_LDS_BLOCK_WIDE
+#define RT_LDS_BLOCK_WIDE 512
+#endif
+constexpr uint32_t trace_threads(bool lds, int mesh, int kind) {
+    return !lds ? 256u : mesh == 3 ? (uint32_t)RT_LDS_BLOCK_WIDE : mesh ? (uint32_t)RT_LDS_BLOCK_MESH
                        : kind == 0 ? (uint32_t)RT_LDS_BLOCK_SPHERES : (uint32_t)RT_LDS_BLOCK_SPHERES_AUX;
 }
-constexpr int trace_waves_per_eu(bool lds, bool mesh, int kind) {
-    return kind != 0 ? RT_WAVES_PER_EU : mesh ? RT_WAVES_PER_EU_MESH
+constexpr int trace_waves_per_eu(bool lds, int mesh, int kind) {
+    return kind != 0 ? RT_WAVES_PER_EU : mesh == 3 ? RT_WAVES_PER_EU_WIDE : mesh ? RT_WAVES_PER_EU_MESH
                        : lds ? RT_WAVES_PER_EU_SPHERES : RT_WAVES_PER_EU_SPHERES_GLOBAL;
 }
 template <bool kBvh, bool kLds, bool kStep, int kMesh, bool kCount, bool kSerial = false>
-__global__ __launch_bounds__(trace_threads(kLds, kMesh != 0, kSerial ? 2 : kCount ? 1 : 0))
-__attribute__((amdgpu_waves_per_eu(trace_waves_per_eu(kLds, kMesh != 0, kSerial ? 2 : kCount ? 1 : 0), 8)))
+__global__ __launch_bounds__(trace_threads(kLds, kMesh, kSerial ? 2 : kCount ? 1 : 0))
+__attribute__((amdgpu_waves_per_eu(trace_waves_per_eu(kLds, kMesh, kSerial ? 2 : kCount ? 1 : 0), 8)))
 void trace_kernel(TraceParams p) {
     // SERIAL count passes: the walk of the previous pass set the first sample
     // and this iteration's candidates per sample (ctrl[5], <= the launch's K)
@@ -872,6 +920,13 @@ void trace_kernel(TraceParams p) {
     extern __shared__ float4 lds[];
     BvhView view;
     const uint32_t sph_root = stage_tree<kLds>(p, lds, view);  // the sphere walk's first node
+    // kMesh 3: the lane's stack of wide-node indices (u16, entry k at
+    // tstack[k * blockDim.x]) after the sphere tree's LDS copy
+    uint16_t *const tstack = reinterpret_cast<uint16_t *>(
+                                 reinterpret_cast<char *>(lds) +
+                                 (kLds ? (trace_tree_lds(p.nnodes, p.nprims, p.nsph_padded) + 15u) & ~(size_t)15u
+                                       : 0u)) + threadIdx.x;
+    uint32_t tsp = 0;  // (kMesh 3) entries on the stack
 
     F3 org = f3(0, 0, 0), dir = f3(0, 0, 0), inv = f3(0, 0, 0);
     float thr_r = 1.0f, thr_g = 1.0f, thr_b = 1.0f;  // ray_color's final_color
@@ -1052,8 +1107,9 @@ void trace_kernel(TraceParams p) {
                 phase = kShade;
                 if (kMesh == 0) {
                     // no triangles: Mesh::hit finds nothing
-                } else if (kMesh == 2) {  // (p.tnodes != 0)
-                    const bool cam = bounce == 0 && p.cam_nnodes != 0;
+                } else if (kMesh >= 2) {  // (p.tnodes != 0)
+                    // (kMesh 3: every lane walks the static tree's wide image)
+                    const bool cam = kMesh == 2 && bounce == 0 && p.cam_nnodes != 0;
                     if (tri_begin(p, org, dir, best_t, cam, e, tri_t, tri_i, tri_in, tri_done)) {
                         // (the lists index the camera-origin records, which exist
                         // without the camera tree's nodes: runtime.cpp prepare_camera)
@@ -1062,6 +1118,7 @@ void trace_kernel(TraceParams p) {
                                              tri_done);
                         } else {
                             node = 0;
+                            tsp = 0;
                             phase = kTri;
                         }
                     }
@@ -1070,7 +1127,7 @@ void trace_kernel(TraceParams p) {
                 }
             }
             bool tri_now = true;
-            if (kMesh == 2 && p.tri_walk_min != 0) {
+            if (kMesh >= 2 && p.tri_walk_min != 0) {
                 const uint32_t nwalk = (uint32_t)__popcll(__ballot(phase == kTri));
                 const uint32_t nother = (uint32_t)__popcll(__ballot(phase != kTri && !done));
                 tri_now = nwalk >= p.tri_walk_min || nother == 0;
@@ -1093,6 +1150,83 @@ void trace_kernel(TraceParams p) {
                     }
                 } while (node != kNodeEndDev && (!kStep || --budget != 0));
                 if (node == kNodeEndDev) phase = kShade;
+            }
+            if (kMesh == 3 && phase == kTri && tri_now) {
+                // The static tree's 4-wide image: one 128-B record per step
+                // holds four children's boxes (one round trip where the binary
+                // walk takes about four; tools/tbvh_sim.cpp SIM_WIDE=4: 584 ->
+                // 146 dependent node loads per secondary ray, the same box
+                // tests).  Leaf children are tested at once; of the internal
+                // children that are entered, the lowest slot is walked next and
+                // the others are pushed on the lane's LDS stack.  Any order is
+                // exact (tri_merge keeps the (t, index) argmin).
+                const TraceParams &p = kargs();  // (see kargs)
+                uint32_t wbudget = p.wsteps;
+                const F3 dlt2 = f3(2.0f * (org.x - p.tbvh_oc[0]), 2.0f * (org.y - p.tbvh_oc[1]),
+                                   2.0f * (org.z - p.tbvh_oc[2]));
+                F3 nlo, nhi;
+                sphere_slabs(org, inv, e, nlo, nhi);
+                float cap = fminf(best_t, tri_t);
+                do {
+                    const uint4 *wn = p.tw_nodes + 8u * node;
+                    tnode_tests += 4;
+                    float tn[4];
+                    bool in[4];
+#ifndef RT_WIDE_ONE_LOAD
+                    // two halves: the first brings the 128-B line into the L1,
+                    // the second (after a compiler barrier, so that the node
+                    // never occupies 28 VGPRs at once) hits it there
+                    {
+                        const uint4 q0 = wn[0], q1 = wn[1], q2 = wn[2];
+                        in[0] = tri_wide_child(p, q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, nlo, nhi, inv, dlt2, cap, tn[0]);
+                        in[1] = tri_wide_child(p, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w, nlo, nhi, inv, dlt2, cap, tn[1]);
+                    }
+                    asm volatile("" ::: "memory");
+                    {
+                        const uint4 q3 = wn[3], q4 = wn[4], q5 = wn[5];
+                        in[2] = tri_wide_child(p, q3.x, q3.y, q3.z, q3.w, q4.x, q4.y, nlo, nhi, inv, dlt2, cap, tn[2]);
+                        in[3] = tri_wide_child(p, q4.z, q4.w, q5.x, q5.y, q5.z, q5.w, nlo, nhi, inv, dlt2, cap, tn[3]);
+                    }
+#else
+                    {
+                        const uint4 q0 = wn[0], q1 = wn[1], q2 = wn[2], q3 = wn[3], q4 = wn[4], q5 = wn[5];
+                        in[0] = tri_wide_child(p, q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, nlo, nhi, inv, dlt2, cap, tn[0]);
+                        in[1] = tri_wide_child(p, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w, nlo, nhi, inv, dlt2, cap, tn[1]);
+                        in[2] = tri_wide_child(p, q3.x, q3.y, q3.z, q3.w, q4.x, q4.y, nlo, nhi, inv, dlt2, cap, tn[2]);
+                        in[3] = tri_wide_child(p, q4.z, q4.w, q5.x, q5.y, q5.z, q5.w, nlo, nhi, inv, dlt2, cap, tn[3]);
+                    }
+#endif
+                    const uint4 qa = wn[6];
+                    const uint32_t a[4] = {qa.x, qa.y, qa.z, qa.w};
+                    // entered leaf children, one copy of the leaf test for all four
+                    uint32_t lmask = 0;
+#pragma unroll
+                    for (int c = 0; c < 4; ++c) lmask |= (in[c] && (a[c] & kLeafBitDev)) ? 1u << c : 0u;
+                    while (lmask != 0) {
+                        const uint32_t c = (uint32_t)__builtin_ctz(lmask);
+                        lmask &= lmask - 1u;
+                        const uint32_t lw = c == 0 ? a[0] : c == 1 ? a[1] : c == 2 ? a[2] : a[3];
+                        tri_leaf(p, org, dir, false, lw & ~kLeafBitDev, best_t, tri_t, tri_i, tri_in, tri_done);
+                    }
+                    cap = fminf(best_t, tri_t);
+                    uint32_t nxt = 0xFFFFu;
+#pragma unroll
+                    for (int c = 3; c >= 0; --c) {
+                        if (in[c] && !(a[c] & kLeafBitDev) && __float_as_int(tn[c]) <= __float_as_int(cap)) {
+                            if (nxt != 0xFFFFu) {
+                                tstack[tsp * blockDim.x] = (uint16_t)nxt;
+                                ++tsp;
+                            }
+                            nxt = a[c];
+                        }
+                    }
+                    if (nxt == 0xFFFFu && tsp != 0) {
+                        --tsp;
+                        nxt = tstack[tsp * blockDim.x];
+                    }
+                    node = nxt;
+                } while (node != 0xFFFFu && (!kStep || --wbudget != 0));
+                if (node == 0xFFFFu) phase = kShade;
             }
             RT_STAMP(2);
             if (phase == kShade) {
@@ -1228,7 +1362,7 @@ void trace_kernel(TraceParams p) {
                     if (n != 0 && rleft[k] == 0) {
                         const TraceParams &pc = kargs();
                         if (!(pc.ablate & 2u))
-                            resolve_chunk<kMesh != 2>(pc, sbase, pstride, k << pc.ring_shift, rbase[k],
+                            resolve_chunk<kMesh < 2>(pc, sbase, pstride, k << pc.ring_shift, rbase[k],
                                                   rlen[k], lane);
                         rfree |= 1u << k;
                     }
@@ -1448,26 +1582,31 @@ __global__ __launch_bounds__(kResolveWaves * 64) void resolve_kernel(
 
 }  // namespace
 
-uint32_t trace_block_threads(bool lds, bool mesh, int kind) { return trace_threads(lds, mesh, kind); }
+uint32_t trace_block_threads(bool lds, int mesh, int kind) { return trace_threads(lds, mesh, kind); }
 
 size_t trace_lds_bytes(const TraceParams &p) {
     // (shading records in global memory instead, which would allow 8 waves per
     // SIMD: A/B +1.7 % at 6 waves, +8 % at 8 waves per SIMD)
-    return (size_t)p.nnodes * 48 + (size_t)p.nprims * 20 + (size_t)p.nsph_padded * 36;
+    return trace_tree_lds(p.nnodes, p.nprims, p.nsph_padded);
+}
+
+size_t trace_dyn_lds(const TraceParams &p, bool lds, bool wide, uint32_t threads) {
+    const size_t tree = lds ? (trace_lds_bytes(p) + 15u) & ~(size_t)15u : 0u;
+    return tree + (wide ? (size_t)p.tw_depth * threads * 2u : 0u);
 }
 
 template <bool kStep, int kMesh, bool kCount, bool kSerial>
 static void launch_trace_t(const TraceParams &p, uint32_t blocks, hipStream_t stream) {
+    const uint32_t lt = trace_threads(true, kMesh, kSerial ? 2 : kCount ? 1 : 0);
     if (p.nnodes && p.use_lds)
-        hipLaunchKernelGGL((trace_kernel<true, true, kStep, kMesh, kCount, kSerial>), dim3(blocks),
-                           dim3(trace_threads(true, kMesh != 0, kSerial ? 2 : kCount ? 1 : 0)),
-                           trace_lds_bytes(p), stream, p);
+        hipLaunchKernelGGL((trace_kernel<true, true, kStep, kMesh, kCount, kSerial>), dim3(blocks), dim3(lt),
+                           trace_dyn_lds(p, true, kMesh == 3, lt), stream, p);
     else if (p.nnodes)
         hipLaunchKernelGGL((trace_kernel<true, false, kStep, kMesh, kCount, kSerial>), dim3(blocks),
-                           dim3(256), 0, stream, p);
+                           dim3(256), trace_dyn_lds(p, false, kMesh == 3, 256), stream, p);
     else
         hipLaunchKernelGGL((trace_kernel<false, false, kStep, kMesh, kCount, kSerial>), dim3(blocks),
-                           dim3(256), 0, stream, p);
+                           dim3(256), trace_dyn_lds(p, false, kMesh == 3, 256), stream, p);
 }
 
 // kMesh: 0 no triangles, 1 brute-force triangles (no triangle tree: small
@@ -1475,6 +1614,11 @@ static void launch_trace_t(const TraceParams &p, uint32_t blocks, hipStream_t st
 template <bool kCount, bool kSerial>
 static void launch_trace_c(const TraceParams &p, uint32_t blocks, hipStream_t stream) {
     const int mesh = trace_mesh_kind(p.ntri != 0, p.tnodes != 0);
+    if (!kSerial && mesh == 2 && p.tw_nodes != nullptr) {
+        if (p.step) launch_trace_t<true, 3, kCount, false>(p, blocks, stream);
+        else launch_trace_t<false, 3, kCount, false>(p, blocks, stream);
+        return;
+    }
     if (p.step) {
         if (mesh == 2) launch_trace_t<true, 2, kCount, kSerial>(p, blocks, stream);
         else if (mesh == 1) launch_trace_t<true, 1, kCount, kSerial>(p, blocks, stream);
@@ -1511,17 +1655,21 @@ static hipError_t trace_occupancy_t(int *blocks_per_cu, int variant, size_t lds_
     if (variant == 2)
         return hipOccupancyMaxActiveBlocksPerMultiprocessor(
             blocks_per_cu, trace_kernel<true, true, kStep, kMesh, kCount, kSerial>,
-            trace_threads(true, kMesh != 0, kind), lds_bytes);
+            trace_threads(true, kMesh, kind), lds_bytes);
     if (variant == 1)
         return hipOccupancyMaxActiveBlocksPerMultiprocessor(
-            blocks_per_cu, trace_kernel<true, false, kStep, kMesh, kCount, kSerial>, 256, 0);
+            blocks_per_cu, trace_kernel<true, false, kStep, kMesh, kCount, kSerial>, 256, lds_bytes);
     return hipOccupancyMaxActiveBlocksPerMultiprocessor(
-        blocks_per_cu, trace_kernel<false, false, kStep, kMesh, kCount, kSerial>, 256, 0);
+        blocks_per_cu, trace_kernel<false, false, kStep, kMesh, kCount, kSerial>, 256, lds_bytes);
 }
 
 template <bool kCount, bool kSerial>
 static hipError_t trace_occupancy_c(int *blocks_per_cu, int variant, size_t lds_bytes, bool step,
                                     int mesh) {
+    if (!kSerial && mesh == 3)
+        return step ? trace_occupancy_t<true, 3, kCount, false>(blocks_per_cu, variant, lds_bytes)
+                    : trace_occupancy_t<false, 3, kCount, false>(blocks_per_cu, variant, lds_bytes);
+    if (mesh == 3) mesh = 2;
     if (step)
         return mesh == 2   ? trace_occupancy_t<true, 2, kCount, kSerial>(blocks_per_cu, variant, lds_bytes)
                : mesh == 1 ? trace_occupancy_t<true, 1, kCount, kSerial>(blocks_per_cu, variant, lds_bytes)

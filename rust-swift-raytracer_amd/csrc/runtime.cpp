@@ -51,7 +51,7 @@ DeviceState::~DeviceState() {
     if (hipSetDevice(device) != hipSuccess) return;
     void *bufs[] = {sph_hot, sph_cold, tri_hot, tri_geo, mats, samples, ring, out, replay, counter, stats,
                     bvh_nodes, bvh_prims, big_hot, bvh_miss, bvh_prim_id, big_id, bvh_miss16,
-                    sph_shade, sph_kind, tbvh_nodes, tbvh_tris, tbvh_loose,
+                    sph_shade, sph_kind, tbvh_nodes, tbvh_tris, tbvh_loose, tw_nodes,
                     cam_nodes, cam_tris, ptl_off, ptl_items, spl, tile, gath,
                     sstates, stab, sscan, swin, sjump, sctrl, sbend, spath, sfin,
                     gspl, gspl_rects, gspl_flag, scheck, slo, ssbend, ssb, sptab};
@@ -110,11 +110,22 @@ static int device_for(WorldState &w, int want, DeviceState *&out) {
         d->num_cus = prop.multiProcessorCount;
         // the scene's kernel family (render.h trace_mesh_kind; frames rendered with
         // RT_ACCEL_BRUTE run the brute-force triangle kernels on these figures)
-        const int tri = trace_mesh_kind(w.packed.ntri > 0, !w.tbvh.nodes.empty());
+        // Triangle trees are walked through their 4-wide image (kMesh 3) when it
+        // exists and every lane's stack fits in LDS beside a workgroup's tree
+        // (RT_AMD_TRI_WIDE=0: the binary walk)
+        const TriangleBVH &tw = w.tbvh;
+        const uint32_t tw_depth = std::max<uint32_t>(1u, 3u * tw.wdepth);
+        const bool wide = !tw.wnodes.empty() && env_u64("RT_AMD_TRI_WIDE", 1) != 0 &&
+                          (size_t)tw_depth * trace_block_threads(true, 3, 0) * 2u <= 64u * 1024u;
+        const int tri = wide ? 3 : trace_mesh_kind(w.packed.ntri > 0, !w.tbvh.nodes.empty());
+        // the stack's LDS (kinds 0 and 1: SERIAL passes keep the binary walk)
+        auto stack_lds = [&](int c, uint32_t threads) -> size_t {
+            return tri == 3 && c != 2 ? (size_t)tw_depth * threads * 2u : 0u;
+        };
         for (int c = 0; c < 3; ++c)
             for (int st = 0; st < 2; ++st) {
-                HIP_TRY(trace_occupancy(&d->blocks_per_cu[c][st], 0, 0, st, tri, c));
-                HIP_TRY(trace_occupancy(&d->blocks_per_cu_bvh[c][st], 1, 0, st, tri, c));
+                HIP_TRY(trace_occupancy(&d->blocks_per_cu[c][st], 0, stack_lds(c, 256), st, tri, c));
+                HIP_TRY(trace_occupancy(&d->blocks_per_cu_bvh[c][st], 1, stack_lds(c, 256), st, tri, c));
             }
         // scene upload (once per device)
         const PackedScene &p = w.packed;
@@ -168,7 +179,10 @@ static int device_for(WorldState &w, int want, DeviceState *&out) {
                 bool fits = true;
                 for (int c = 0; c < 3; ++c)
                     for (int st = 0; st < 2; ++st) {
-                        HIP_TRY(trace_occupancy(&d->blocks_per_cu_lds[c][st], 2, lds, st, tri, c));
+                        const uint32_t lt = trace_block_threads(true, tri == 3 && c == 2 ? 2 : tri, c);
+                        const size_t sb = stack_lds(c, lt);
+                        HIP_TRY(trace_occupancy(&d->blocks_per_cu_lds[c][st], 2,
+                                                sb ? ((lds + 15u) & ~(size_t)15u) + sb : lds, st, tri, c));
                         fits = fits && d->blocks_per_cu_lds[c][st] > 0;
                     }
                 if (fits) d->lds_bytes = lds;
@@ -185,6 +199,10 @@ static int device_for(WorldState &w, int want, DeviceState *&out) {
             HIP_TRY(up((void **)&d->tbvh_tris, tb.tris));
             HIP_TRY(upu((void **)&d->tbvh_loose, tb.loose));
             d->tnodes = (uint32_t)(tb.qnodes.size() / 8);
+            if (wide) {
+                HIP_TRY(upu((void **)&d->tw_nodes, tb.wnodes));
+                d->tw_depth = tw_depth;
+            }
             d->ttris = (uint32_t)(tb.tris.size() / 16);
             d->tloose = (uint32_t)tb.loose.size();
         }
@@ -534,6 +552,13 @@ int render_frame(WorldState &w, const CameraModel &cam, size_t width, size_t hei
         }
         p.tq_nbase = tb.nbase;
         p.tq_nstep = tb.nstep;
+        if (d->tw_nodes) {
+            p.tw_nodes = d->tw_nodes;
+            p.tw_depth = d->tw_depth;
+            // wide-node fetches per lane per loop iteration of a sliced walk (A/B
+            // on C5: 16 -> 166.1 ms, 20 -> 163.9, 24 -> 163.5, 28 -> 164.4, 32 -> 166.4)
+            p.wsteps = (uint32_t)std::max<uint64_t>(1, env_u64("RT_AMD_WSTEPS", 24));
+        }
         p.tbvh_r = tb.radius; p.tbvh_mag = tb.mag;
     }
     const float inv_spp = 1.0f / (float)o.samples_per_pixel;  // 1.0 / spp as f32 (common.rs:345)
@@ -564,7 +589,9 @@ int render_frame(WorldState &w, const CameraModel &cam, size_t width, size_t hei
     const int bpc = !use_bvh   ? d->blocks_per_cu[ctv][sv]
                     : p.use_lds ? d->blocks_per_cu_lds[ctv][sv]
                                 : d->blocks_per_cu_bvh[ctv][sv];
-    const uint64_t waves_per_block = trace_block_threads(use_bvh && p.use_lds, p.ntri != 0, ctv) / 64;
+    // (the kernel family launch_trace picks: the wide triangle walk for frames)
+    const int fam = p.ntri == 0 ? 0 : p.tnodes == 0 ? 1 : (p.tw_nodes != nullptr && ctv != 2) ? 3 : 2;
+    const uint64_t waves_per_block = trace_block_threads(use_bvh && p.use_lds, fam, ctv) / 64;
     const uint64_t full_blocks = (uint64_t)bpc * (uint64_t)d->num_cus;
     double trace_ms = 0.0, resolve_ms = 0.0;
     uint32_t launches = 0, waves = 0;

@@ -43,6 +43,8 @@ struct DeviceState {
     float4 *tbvh_tris = nullptr;
     uint32_t *tbvh_loose = nullptr;
     uint32_t tnodes = 0, ttris = 0, tloose = 0;
+    uint4 *tw_nodes = nullptr;                                  // its 4-wide image (bvh.h wnodes)
+    uint32_t tw_depth = 0;                                      // stack entries per lane
     uint4 *cam_nodes = nullptr;                                 // camera-origin triangle BVH
     float4 *cam_tris = nullptr;
     uint32_t cam_nnodes = 0;

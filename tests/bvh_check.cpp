@@ -11,6 +11,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <map>
 #include <fstream>
 #include <sstream>
 #include <vector>
@@ -108,6 +109,61 @@ static void check_quant(const std::vector<float> &nodes, size_t stride, const st
     }
 }
 
+// The 4-wide image (bvh.h TriangleBVH::wnodes): a walk of every slot reaches
+// each wide node once and each binary leaf's word once, every child's box
+// words are a binary node's, and the stack bound holds (3 * wdepth).
+static void check_wide(const TriangleBVH &tb) {
+    const size_t nw = tb.wnodes.size() / 32, nq = tb.qnodes.size() / 8;
+    CHECK(nw > 0 && tb.wnodes.size() == nw * 32 && nw <= 65535, "wide: %zu records\n", nw);
+    if (nw == 0) return;
+    std::vector<int> seen(nw, 0);
+    std::map<uint32_t, int> leaves;
+    std::map<std::vector<uint32_t>, std::vector<uint32_t>> words;  // words 0-5 -> leaf words (0: internal)
+    for (size_t i = 0; i < nq; ++i) {
+        const uint32_t *q = &tb.qnodes[i * 8];
+        words[std::vector<uint32_t>(q, q + 6)].push_back((q[6] & kLeafBit) ? q[6] : 0u);
+    }
+    std::vector<std::pair<uint32_t, uint32_t>> st{{0u, 0u}};  // (wide node, depth)
+    size_t maxstack = 0;
+    while (!st.empty()) {
+        const auto [w, dpt] = st.back();
+        st.pop_back();
+        CHECK(w < nw, "wide: index %u out of range\n", w);
+        if (w >= nw) return;
+        seen[w]++;
+        CHECK(dpt <= tb.wdepth, "wide: node %u deeper (%u) than wdepth %u\n", w, dpt, tb.wdepth);
+        const uint32_t *r = &tb.wnodes[(size_t)w * 32];
+        size_t pushed = 0;
+        for (int c = 0; c < 4; ++c) {
+            const uint32_t a = r[24 + c];
+            if (a == kLeafBit) continue;  // empty slot
+            // the slot's words are some binary node's words 0-5 (and its leaf word)
+            bool found = false;
+            auto it = words.find(std::vector<uint32_t>(r + 6 * c, r + 6 * c + 6));
+            if (it != words.end())
+                for (uint32_t lw : it->second) found = found || lw == ((a & kLeafBit) ? a : 0u);
+            CHECK(found, "wide: node %u slot %d is no binary node\n", w, c);
+            if (a & kLeafBit) {
+                leaves[a]++;
+            } else {
+                st.push_back({a, dpt + 1});
+                ++pushed;
+            }
+        }
+        maxstack = std::max(maxstack, st.size());
+        (void)pushed;
+    }
+    for (size_t i = 0; i < nw; ++i) CHECK(seen[i] == 1, "wide: node %zu reached %d times\n", i, seen[i]);
+    size_t nleaf = 0;
+    for (size_t i = 0; i < nq; ++i)
+        if (tb.qnodes[i * 8 + 6] & kLeafBit) {
+            ++nleaf;
+            CHECK(leaves[tb.qnodes[i * 8 + 6]] == 1, "wide: leaf %zu reached %d times\n", i,
+                  leaves[tb.qnodes[i * 8 + 6]]);
+        }
+    CHECK(leaves.size() == nleaf, "wide: %zu leaf words, %zu binary leaves\n", leaves.size(), nleaf);
+}
+
 int main(int argc, char **argv) {
     std::ifstream fh(argv[1]);
     std::stringstream ss;
@@ -127,6 +183,7 @@ int main(int argc, char **argv) {
         check_tree(tb.nodes, 16, tb.tris.size() / 16, leaf, "static");
         check_links(tb.nodes, 16, tb.miss, "static");
         check_quant(tb.nodes, 16, tb.qnodes, tb.miss, tb.qbox, tb.nbase, tb.nstep, "static");
+        check_wide(tb);
         const float o[3] = {s.camera.origin.x, s.camera.origin.y, s.camera.origin.z};
         cb = build_camera_triangle_bvh(s.triangles, p.tri_hot, tb, o, leaf);
         check_tree(cb.nodes, 8, cb.tris.size() / 16, leaf, "camera");

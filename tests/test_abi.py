@@ -169,8 +169,8 @@ def test_render_null_arguments_return_empty_framebuffer():
 
 def test_frame_kernel_hash_covers_the_lean_frame_kernels():
     """bench.py keys roofline.traffic on tools/kernel_hash.py: the gfx950 code
-    of the 18 lean frame variants of trace_kernel inside the built library
-    (3 sphere searches x 2 walk kinds x 3 mesh kinds), found in the offload
+    of the 24 lean frame variants of trace_kernel inside the built library
+    (3 sphere searches x 2 walk kinds x 4 mesh kinds), found in the offload
     bundle; the hash is stable across reads."""
     import sys
 
@@ -178,6 +178,6 @@ def test_frame_kernel_hash_covers_the_lean_frame_kernels():
     import kernel_hash
 
     digest, names = kernel_hash.frame_kernel_hash(R.LIB_PATH)
-    assert len(names) == 18 and all("trace_kernel" in n for n in names)
+    assert len(names) == 24 and all("trace_kernel" in n for n in names)
     assert re.fullmatch(r"[0-9a-f]{64}", digest)
     assert kernel_hash.frame_kernel_hash(R.LIB_PATH)[0] == digest

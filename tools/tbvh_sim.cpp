@@ -140,6 +140,156 @@ static float trace(const TriangleBVH &t, V o, V d, Count &c) {
     return best;
 }
 
+// SIM_WIDE=K: the static tree collapsed to K-wide nodes (each node's K child
+// boxes fetched together: one dependent round trip per node), walked with a
+// per-ray stack, hit children nearest-first, leaves tested as their box is hit.
+// Child boxes are the binary image's (same decode and widening arithmetic).
+struct Wide {
+    std::vector<std::vector<uint32_t>> kids;  // per binary node index: its wide children
+};
+static float qarea(const TriangleBVH &t, uint32_t n) {
+    const uint32_t *w = &t.qnodes[(size_t)n * 8];
+    float e[3];
+    for (int k = 0; k < 3; ++k) {
+        const uint32_t lo = (w[k] & 0xFFFF), hi = w[k] >> 16;
+        (void)lo; (void)hi;
+    }
+    const uint32_t u[6] = {w[0] & 0xFFFF, w[0] >> 16, w[1] & 0xFFFF, w[1] >> 16, w[2] & 0xFFFF, w[2] >> 16};
+    for (int k = 0; k < 3; ++k) e[k] = (float)(u[3 + k] - u[k]) * t.qbox.step[k];
+    return e[0] * e[1] + e[1] * e[2] + e[0] * e[2];
+}
+static Wide make_wide(const TriangleBVH &t, int K) {
+    Wide W;
+    const size_t n = t.qnodes.size() / 8;
+    W.kids.resize(n);
+    for (size_t i = 0; i < n; ++i) {
+        const uint32_t a = t.qnodes[i * 8 + 6];
+        if (a & kLeafBit) continue;
+        std::vector<uint32_t> k{a & 0x1FFFFFFFu, (a & 0x1FFFFFFFu) + 1};
+        static const bool level = std::getenv("SIM_WIDE_LEVEL") != nullptr;  // grandchildren, not largest-area
+        while ((int)k.size() < K) {
+            int best = -1;
+            float ba = -1;
+            for (size_t j = 0; j < k.size(); ++j) {
+                if (t.qnodes[(size_t)k[j] * 8 + 6] & kLeafBit) continue;
+                if (level && j >= 2) break;
+                const float ar = level ? 1.0f : qarea(t, k[j]);
+                if (ar > ba) { ba = ar; best = (int)j; }
+            }
+            if (best < 0) break;
+            const uint32_t c = t.qnodes[(size_t)k[best] * 8 + 6] & 0x1FFFFFFFu;
+            k.erase(k.begin() + best);
+            k.push_back(c);
+            k.push_back(c + 1);
+        }
+        W.kids[i] = k;
+    }
+    // wide nodes reachable from the root, their depth, the stack bound
+    std::vector<std::pair<uint32_t, int>> st{{0u, 0}};
+    size_t nw = 0;
+    int maxd = 0;
+    while (!st.empty()) {
+        auto [i, dd] = st.back();
+        st.pop_back();
+        ++nw;
+        maxd = std::max(maxd, dd);
+        for (uint32_t c : W.kids[i])
+            if (!(t.qnodes[(size_t)c * 8 + 6] & kLeafBit)) st.push_back({c, dd + 1});
+    }
+    std::printf("wide K=%d: %zu wide nodes, max depth %d (stack bound %d)\n", K, nw, maxd, (K - 1) * maxd);
+    return W;
+}
+struct WideCount { double fetches = 0, boxes = 0, tests = 0, rays = 0, maxstack = 0, pops = 0; };
+static float trace_wide(const TriangleBVH &t, const Wide &W, V o, V d, WideCount &c) {
+    c.rays += 1;
+    const float onorm = std::fabs(o.x) + std::fabs(o.y) + std::fabs(o.z);
+    const float iv[3] = {1.0f / d.x, 1.0f / d.y, 1.0f / d.z};
+    const float dist = std::fabs(o.x - t.centre[0]) + std::fabs(o.y - t.centre[1]) +
+                       std::fabs(o.z - t.centre[2]) + t.radius + 2 * onorm;
+    const float rho = 1e-5f * (dist + onorm + t.mag);
+    const float ov[3] = {o.x, o.y, o.z};
+    const float dv[3] = {o.x - t.oc[0], o.y - t.oc[1], o.z - t.oc[2]};
+    auto dec = [](uint32_t q, float s, float b) { return std::fmaf((float)q, s, b); };
+    auto box = [&](uint32_t node, float &tn, float &tf) {
+        const uint32_t *w = &t.qnodes[(size_t)node * 8];
+        const uint32_t u[6] = {w[0] & 0xFFFF, w[0] >> 16, w[1] & 0xFFFF, w[1] >> 16, w[2] & 0xFFFF, w[2] >> 16};
+        const uint32_t m[6] = {w[3] & 0xFFFF, w[3] >> 16, w[4] & 0xFFFF, w[4] >> 16, w[5] & 0xFFFF, w[5] >> 16};
+        float sl = 0, sh = 0, n0[3], n1[3];
+        for (int k = 0; k < 3; ++k) {
+            n0[k] = dec(m[k], t.nstep, t.nbase);
+            n1[k] = dec(m[3 + k], t.nstep, t.nbase);
+            float a = n0[k] * dv[k], b = n1[k] * dv[k];
+            sl += std::fmin(a, b); sh += std::fmax(a, b);
+        }
+        tn = -INFINITY; tf = INFINITY;
+        for (int k = 0; k < 3; ++k) {
+            float a = sl * n0[k], b = sl * n1[k], cc = sh * n0[k], dd = sh * n1[k];
+            float lo = dec(u[k], t.qbox.step[k], t.qbox.base[k]) + 2 * std::fmin(std::fmin(a, b), std::fmin(cc, dd)) - rho;
+            float hi = dec(u[3 + k], t.qbox.step[k], t.qbox.base[k]) + 2 * std::fmax(std::fmax(a, b), std::fmax(cc, dd)) + rho;
+            float t0 = (lo - ov[k]) * iv[k], t1 = (hi - ov[k]) * iv[k];
+            tn = std::fmax(tn, std::fmin(t0, t1));
+            tf = std::fmin(tf, std::fmax(t0, t1));
+        }
+    };
+    float best = INFINITY;
+    auto leaf = [&](uint32_t a) {
+        const uint32_t first = (a & ~kLeafBit) >> 3, count = a & 7u;
+        for (uint32_t j = first; j < first + count; ++j) {
+            c.tests += 1;
+            const float *r = &t.tris[(size_t)j * 16];
+            V N{r[0], r[1], r[2]};
+            float cs = dot(N, d);
+            if (std::fabs(cs) < 1e-8f) continue;
+            float tt = (dot(N, o) + r[3]) / cs;
+            if (tt < 0.001f || tt > best) continue;
+            V pp = add(o, mul(d, tt));
+            V v0{r[4], r[5], r[6]}, v1{r[8], r[9], r[10]}, v2{r[12], r[13], r[14]};
+            if (dot(N, cross(sub(v1, v0), sub(pp, v0))) < 0) continue;
+            if (dot(N, cross(sub(v2, v1), sub(pp, v1))) < 0) continue;
+            if (dot(N, cross(sub(v0, v2), sub(pp, v2))) < 0) continue;
+            best = tt;
+        }
+    };
+    // the root's own box first (as the binary walk does)
+    {
+        float tn, tf;
+        c.boxes += 1;
+        box(0, tn, tf);
+        if (tn > tf || tf < 0.001f) return best;
+        const uint32_t a = t.qnodes[6];
+        if (a & kLeafBit) { leaf(a); return best; }
+    }
+    std::vector<std::pair<float, uint32_t>> st{{-INFINITY, 0u}};
+    while (!st.empty()) {
+        const auto [etn, node] = st.back();
+        st.pop_back();
+        c.pops += 1;
+        if (etn > best) continue;
+        c.fetches += 1;
+        std::vector<std::pair<float, uint32_t>> hits;
+        for (uint32_t ch : W.kids[node]) {
+            float tn, tf;
+            c.boxes += 1;
+            box(ch, tn, tf);
+            if (tn > tf || tf < 0.001f || tn > best) continue;
+            hits.push_back({tn, ch});
+        }
+        // SIM_WIDE_ORDER=0: slot order (nearest-first otherwise)
+        static const bool sorted = !std::getenv("SIM_WIDE_ORDER") || std::atoi(std::getenv("SIM_WIDE_ORDER")) != 0;
+        if (sorted) std::sort(hits.begin(), hits.end());
+        for (auto &h : hits) {
+            const uint32_t a = t.qnodes[(size_t)h.second * 8 + 6];
+            if (a & kLeafBit) { if (h.first <= best) leaf(a); }
+        }
+        for (auto it = hits.rbegin(); it != hits.rend(); ++it) {
+            const uint32_t a = t.qnodes[(size_t)it->second * 8 + 6];
+            if (!(a & kLeafBit) && it->first <= best) st.push_back(*it);
+        }
+        c.maxstack = std::max(c.maxstack, (double)st.size());
+    }
+    return best;
+}
+
 // SIM_Q8=B[,N]: 16-B nodes.  The tree in DFS preorder (first child = next
 // node, skip = + subtree size); blocks of B consecutive nodes carry a float
 // frame (box base + step per axis; normal base + step: one for all axes, or
@@ -415,6 +565,10 @@ int main(int argc, char **argv) {
     }
     V org{cm.origin.x, cm.origin.y, cm.origin.z};
     Count prim, sec, q8c;
+    std::unique_ptr<Wide> wide;
+    WideCount wprim, wsec;
+    size_t wdiff = 0;
+    if (const char *ws = std::getenv("SIM_WIDE")) wide = std::make_unique<Wide>(make_wide(t, std::atoi(ws)));
     std::unique_ptr<Q8> q8;
     size_t q8diff = 0;
     if (const char *qs = std::getenv("SIM_Q8")) {
@@ -432,11 +586,19 @@ int main(int argc, char **argv) {
                                    mul(V{cm.horizontal.x, cm.horizontal.y, cm.horizontal.z}, u)),
                                mul(V{cm.vertical.x, cm.vertical.y, cm.vertical.z}, v)), org));
             float tt = trace(t, org, d, prim);
+            if (wide) {
+                const float tw = trace_wide(t, *wide, org, d, wprim);
+                if (!(tw == tt || (std::isinf(tw) && std::isinf(tt)))) ++wdiff;
+            }
             if (std::isfinite(tt)) {
                 ++hits;
                 V o2 = add(org, mul(d, tt));
                 V d2 = unit(V{rnd() * 2 - 1, rnd() * 2 - 1, rnd() * 2 - 1});
                 const float t2 = trace(t, o2, d2, sec);
+                if (wide) {
+                    const float tw = trace_wide(t, *wide, o2, d2, wsec);
+                    if (!(tw == t2 || (std::isinf(tw) && std::isinf(t2)))) ++wdiff;
+                }
                 if (q8) {
                     const float t3 = trace_q8(t, *q8, o2, d2, q8c);
                     if (!(t2 == t3 || (std::isinf(t2) && std::isinf(t3)))) ++q8diff;
@@ -721,6 +883,12 @@ int main(int argc, char **argv) {
     if (sec.rays)
         std::printf("secondary: %.0f rays, %.1f nodes/ray, %.1f tests/ray\n", sec.rays,
                     sec.nodes / sec.rays, sec.tests / sec.rays);
+    if (wide)
+        for (const WideCount *w : {&wprim, &wsec})
+            std::printf("wide K=%s %s: %.1f fetches/ray, %.1f box tests/ray, %.1f tri tests/ray, "
+                        "%.1f pops/ray, max stack %.0f, %zu hits differ\n", std::getenv("SIM_WIDE"),
+                        w == &wprim ? "primary" : "secondary", w->fetches / w->rays, w->boxes / w->rays,
+                        w->tests / w->rays, w->pops / w->rays, w->maxstack, wdiff);
     if (q8)
         std::printf("q8 B=%d N=%d: secondary %.1f nodes/ray, %.2f frame changes/ray, %.1f tests/ray, %zu hits differ\n",
                     q8->B, q8->N, q8c.nodes / q8c.rays, g_q8_hdr / q8c.rays, q8c.tests / q8c.rays, q8diff);
