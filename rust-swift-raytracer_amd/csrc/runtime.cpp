@@ -579,9 +579,16 @@ int render_frame(WorldState &w, const CameraModel &cam, size_t width, size_t hei
     // refilled together start samples of the same pixel and their primary
     // walks stay coherent (A/B on C2: 1 -> 6.16 ms, 8 -> 6.14, 16 -> 6.12,
     // 32 -> 6.10); sliced walks refill every iteration (C5: 32 costs +5 %)
-    p.refill_min = (uint32_t)std::max<uint64_t>(1, env_u64("RT_AMD_REFILL", p.step ? 1 : 24));
+    // The wide triangle walk (frames only; SERIAL passes walk the binary tree):
+    // refill at 16 idle lanes and walk only when no lane can advance without
+    // it (A/B on C5, refill / walk gate: 1 / 32 -> 163.5 ms, 8 / 32 -> 159.7,
+    // 8 / 64 -> 156.8, 12 / 64 -> 153.1, 16 / 64 -> 151.8, 20 / 64 -> 152.2,
+    // 24 / 64 -> 154.6, 32 / 64 -> 164.7)
+    const bool wide_frame = p.tw_nodes != nullptr && sp == nullptr;
+    p.refill_min = (uint32_t)std::max<uint64_t>(
+        1, env_u64("RT_AMD_REFILL", wide_frame ? 16 : p.step ? 1 : 24));
     p.walk_min = (uint32_t)env_u64("RT_AMD_WALK_MIN", 65);  // sphere-only: walk when nothing else can advance
-    p.tri_walk_min = (uint32_t)env_u64("RT_AMD_TRI_WALK_MIN", 32);
+    p.tri_walk_min = (uint32_t)env_u64("RT_AMD_TRI_WALK_MIN", wide_frame ? 64 : 32);
     const int sv = p.step ? 1 : 0;
     const bool timed = stats != nullptr;  // HIP-event timing + counters need a host wait
     // launch_trace runs the counting variant iff p.stats, the SERIAL instances for sp
