@@ -493,6 +493,33 @@ TriangleBVH build_triangle_bvh(const std::vector<Triangle> &tris, const std::vec
     return out;
 }
 
+// f16 bits of the largest half <= x (up = false) or the smallest half >= x
+// (up = true), for finite x within the half range (the normal boxes: |x| <= 1)
+static float half_value(uint16_t h) {
+    const int e = (h >> 10) & 31, m = h & 1023;
+    const float v = e == 0 ? std::ldexp((float)m, -24) : std::ldexp((float)(1024 + m), e - 25);
+    return (h & 0x8000) ? -v : v;
+}
+static uint16_t half_round(float x, bool up) {
+    static std::vector<std::pair<float, uint16_t>> table;  // every finite half, ascending
+    if (table.empty()) {
+        for (uint32_t h = 0; h < 65536; ++h)
+            if (((h >> 10) & 31) != 31) table.push_back({half_value((uint16_t)h), (uint16_t)h});
+        std::stable_sort(table.begin(), table.end(),
+                         [](const std::pair<float, uint16_t> &a, const std::pair<float, uint16_t> &b) {
+                             return a.first < b.first;
+                         });
+    }
+    if (up) {
+        auto it = std::lower_bound(table.begin(), table.end(), x,
+                                   [](const std::pair<float, uint16_t> &a, float v) { return a.first < v; });
+        return it == table.end() ? (uint16_t)0x7C00u : it->second;  // (+inf: never for |x| <= 1)
+    }
+    auto it = std::upper_bound(table.begin(), table.end(), x,
+                               [](float v, const std::pair<float, uint16_t> &a) { return v < a.first; });
+    return it == table.begin() ? (uint16_t)0xFC00u : std::prev(it)->second;
+}
+
 void build_wide_image(TriangleBVH &tb) {
     tb.wnodes.clear();
     tb.wdepth = 0;
@@ -542,7 +569,16 @@ void build_wide_image(TriangleBVH &tb) {
                 r[24 + c] = kLeafBit;  // empty: a leaf without triangles
                 continue;
             }
-            for (int k = 0; k < 6; ++k) r[6 * c + k] = word(s[c], k);
+            for (int k = 0; k < 3; ++k) r[6 * c + k] = word(s[c], k);
+            // the normal box as halves, rounded outward from the float box
+            // (render.hip tri_wide_child decodes them with v_cvt_f32_f16)
+            const float *nf = &tb.nodes[(size_t)s[c] * 16];
+            uint16_t h[6];
+            for (int k = 0; k < 3; ++k) {
+                h[k] = half_round(nf[8 + k], false);
+                h[3 + k] = half_round(nf[12 + k], true);
+            }
+            for (int k = 0; k < 3; ++k) r[6 * c + 3 + k] = (uint32_t)h[2 * k] | ((uint32_t)h[2 * k + 1] << 16);
             r[24 + c] = is_leaf(s[c]) ? word(s[c], 6) : next++;
         }
         tb.wdepth = std::max(tb.wdepth, depth[w]);

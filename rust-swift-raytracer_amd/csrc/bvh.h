@@ -76,8 +76,10 @@ struct TriangleBVH {
     QuantGrid qbox;
     float nbase = -1, nstep = 1;    // normal grid (all three axes)
     // 4-wide image of the same tree (render.hip tri_wide): one 128-B record per
-    // wide node, 32 u32: child c's box and normal-box words (qnodes words 0-5 of
-    // the binary node it is) at 6c..6c+5, child words at 24..27 -- internal:
+    // wide node, 32 u32: child c's box words (qnodes words 0-2 of the binary
+    // node it is) at 6c..6c+2, its normal box at 6c+3..6c+5 as six halves
+    // (lo.xyz, hi.xyz, rounded outward from the float normal box), child words
+    // at 24..27 -- internal:
     // the child's wide index; leaf: the qnode leaf word (kLeafBit | first << 3 |
     // count); empty slot: kLeafBit (no triangles) -- and 28..31 zero.  Wide
     // node = a binary node's grandchildren (a leaf child stays itself); the

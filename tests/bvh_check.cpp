@@ -118,11 +118,16 @@ static void check_wide(const TriangleBVH &tb) {
     if (nw == 0) return;
     std::vector<int> seen(nw, 0);
     std::map<uint32_t, int> leaves;
-    std::map<std::vector<uint32_t>, std::vector<uint32_t>> words;  // words 0-5 -> leaf words (0: internal)
+    std::map<std::vector<uint32_t>, std::vector<uint32_t>> words;  // box words 0-2 -> binary nodes
     for (size_t i = 0; i < nq; ++i) {
         const uint32_t *q = &tb.qnodes[i * 8];
-        words[std::vector<uint32_t>(q, q + 6)].push_back((q[6] & kLeafBit) ? q[6] : 0u);
+        words[std::vector<uint32_t>(q, q + 3)].push_back((uint32_t)i);
     }
+    auto half = [](uint32_t h) {
+        const int e = (h >> 10) & 31, m = h & 1023;
+        const float v = e == 0 ? std::ldexp((float)m, -24) : std::ldexp((float)(1024 + m), e - 25);
+        return (h & 0x8000) ? -v : v;
+    };
     std::vector<std::pair<uint32_t, uint32_t>> st{{0u, 0u}};  // (wide node, depth)
     size_t maxstack = 0;
     while (!st.empty()) {
@@ -138,10 +143,23 @@ static void check_wide(const TriangleBVH &tb) {
             const uint32_t a = r[24 + c];
             if (a == kLeafBit) continue;  // empty slot
             // the slot's words are some binary node's words 0-5 (and its leaf word)
+            // the slot is some binary node: its box words, its leaf word, and
+            // halves that contain its float normal box
             bool found = false;
-            auto it = words.find(std::vector<uint32_t>(r + 6 * c, r + 6 * c + 6));
+            auto it = words.find(std::vector<uint32_t>(r + 6 * c, r + 6 * c + 3));
             if (it != words.end())
-                for (uint32_t lw : it->second) found = found || lw == ((a & kLeafBit) ? a : 0u);
+                for (uint32_t i : it->second) {
+                    const uint32_t qa = tb.qnodes[(size_t)i * 8 + 6];
+                    if ((a & kLeafBit) ? qa != a : (qa & kLeafBit) != 0) continue;
+                    const float *f = &tb.nodes[(size_t)i * 16];
+                    const uint32_t *h = r + 6 * c + 3;
+                    const float lo[3] = {half(h[0] & 0xFFFF), half(h[0] >> 16), half(h[1] & 0xFFFF)};
+                    const float hi[3] = {half(h[1] >> 16), half(h[2] & 0xFFFF), half(h[2] >> 16)};
+                    bool in = true;
+                    for (int k = 0; k < 3; ++k) in = in && lo[k] <= f[8 + k] && hi[k] >= f[12 + k] &&
+                                                   hi[k] - lo[k] <= f[12 + k] - f[8 + k] + 2e-3f;
+                    found = found || in;
+                }
             CHECK(found, "wide: node %u slot %d is no binary node\n", w, c);
             if (a & kLeafBit) {
                 leaves[a]++;

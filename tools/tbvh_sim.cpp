@@ -15,6 +15,10 @@
 //   SIM_LEVELS=1      share of visits per tree level
 //   SIM_BIN=P         secondary rays of P-ray pools, waves in arrival order vs
 //                     binned by octant + origin cell (SIM_BIN_KEY, SIM_BIN_CELL)
+//   SIM_WIDE=K        the tree collapsed to K-wide nodes, walked with a stack:
+//                     fetches (dependent node loads) vs box tests per ray
+//                     (SIM_WIDE_LEVEL=1: grandchildren, as bvh.cpp builds it;
+//                     SIM_WIDE_ORDER=0: children in slot order, not nearest-first)
 //   SIM_Q8=B,N        16-B nodes in DFS preorder: N>0 u8 boxes and normal boxes
 //                     on per-block frames (B nodes per block; N=3 per-axis
 //                     normal frames), N=0 u16 boxes with one normal box per
