@@ -1,8 +1,9 @@
 """World-size-2/3 CPU (gloo) tests of the multi-GPU tile path: partition,
 all-gather and reassembly (rust-swift-raytracer_amd/tiles.py, used by
-bench.py).  The per-rank renderer is the oracle in COUNTER mode -- frames are
-independent of how rows are partitioned, so the assembled frame must equal
-the single-process frame bit-for-bit."""
+bench.py).  The per-rank renderer is the oracle in COUNTER mode: each rank
+traces only the image rows the product's row map (rt_tile_row) gives it --
+frames are independent of how rows are partitioned, so the assembled frame
+must equal the single-process frame bit-for-bit."""
 import os
 import socket
 
@@ -31,16 +32,22 @@ def free_port():
 def _worker(rank, nranks, block, port, q):
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank,
                             world_size=nranks)
-    full, _, _ = O.Scene(scene_text("c_raytracer_world.txt")).render(W, H, SPP, DEPTH,
-                                                                      mode=O.RNG_COUNTER)
+    scene = O.Scene(scene_text("c_raytracer_world.txt"))
     rows = R.tile_rows(H, block, rank, nranks)
     mr = tiles.max_tile_rows(H, block, nranks)
     tile = np.zeros((mr, W, 4), np.uint8)
-    for k in range(rows):  # this rank's renderer output (fake: rows of the oracle frame)
-        tile[k] = full[R.tile_row(k, block, rank, nranks)]
+    mine = np.zeros((H, W, 4), np.uint8)
+    for k in range(rows):
+        # image row r (top = 0) is the reference's row H - 1 - r (common.rs:327-331):
+        # render that row alone (row_step = H), into this rank's buffer
+        r = R.tile_row(k, block, rank, nranks)
+        scene.render(W, H, SPP, DEPTH, mode=O.RNG_COUNTER, row_begin=H - 1 - r, row_step=H, out=mine)
+        tile[k] = mine[r]
+    rendered = int(np.count_nonzero(mine.reshape(H, -1).any(axis=1)))
     g = tiles.gather_any(torch.from_numpy(tile.reshape(-1)), nranks)
     img = tiles.assemble(g.numpy(), W, H, block, nranks)
-    q.put((rank, bool(np.array_equal(img, full))))
+    full, _, _ = scene.render(W, H, SPP, DEPTH, mode=O.RNG_COUNTER)
+    q.put((rank, bool(np.array_equal(img, full)) and rendered == rows))
     dist.destroy_process_group()
 
 
