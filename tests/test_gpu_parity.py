@@ -275,7 +275,10 @@ def test_scheduling_knobs_do_not_change_samples(monkeypatch, scene):
                 # walk gating: every iteration walks / walks once 8 lanes wait
                 dict(RT_AMD_WALK_MIN="0"), dict(RT_AMD_WALK_MIN="8", RT_AMD_REFILL="5"),
                 dict(RT_AMD_TRI_WALK_MIN="0"), dict(RT_AMD_TRI_WALK_MIN="65"),
-                dict(RT_AMD_STEP="1", RT_AMD_STEPS="7", RT_AMD_WALK_MIN="65")]:
+                dict(RT_AMD_STEP="1", RT_AMD_STEPS="7", RT_AMD_WALK_MIN="65"),
+                # the wide triangle walk's slices and refill rule
+                dict(RT_AMD_WSTEPS="1"), dict(RT_AMD_WSTEPS="3", RT_AMD_REFILL="1"),
+                dict(RT_AMD_WSTEPS="1000", RT_AMD_TRI_WALK_MIN="0")]:
         for k, v in env.items():
             monkeypatch.setenv(k, v)
         out, _ = render_kept(world, w, h, spp, 8)
@@ -297,7 +300,9 @@ def test_tree_shape_knobs_do_not_change_samples(monkeypatch, scene):
     for env in [dict(RT_AMD_LEAF="1"), dict(RT_AMD_LEAF="3"), dict(RT_AMD_LEAF="7"), dict(RT_AMD_TRI_LEAF="2"),
                 dict(RT_AMD_TRI_LEAF="7"), dict(RT_AMD_CAM_LEAF="1"), dict(RT_AMD_CAM_LEAF="5"),
                 dict(RT_AMD_TRI_PHANTOM="0.5"), dict(RT_AMD_BIG_K="2"),
-                dict(RT_AMD_BIG_K="1e9"), dict(RT_AMD_BIG_K="0")]:
+                dict(RT_AMD_BIG_K="1e9"), dict(RT_AMD_BIG_K="0"),
+                # the binary triangle walk instead of the 4-wide image (read at device init)
+                dict(RT_AMD_TRI_WIDE="0"), dict(RT_AMD_TRI_WIDE="0", RT_AMD_TRI_LEAF="3")]:
         for k, v in env.items():
             monkeypatch.setenv(k, v)
         out, _ = render_kept(R.World(src), w, h, spp, 8)
