@@ -718,12 +718,15 @@ int render_frame(WorldState &w, const CameraModel &cam, size_t width, size_t hei
                 p.ring = d->ring;
             }
             // job-queue partitions: each keeps >= 16 chunks.  Whole-walk
-            // kernels take 16: a wave whose partition is drained probes the
+            // kernels take 8: a wave whose partition is drained probes the
             // others one atomic at a time, so at the end of a launch fewer
-            // partitions drain faster (A/B, C2: 64 -> 5.42 ms, 32 -> 5.38, 16 ->
-            // 5.35, 8 -> 5.36, 4 -> 5.38; 8-rank tile: 0.91 / 0.88 / 0.87 / 0.88
-            // / 0.91 ms).  Sliced walks keep 64 (C5: 16 costs +1.6 %).
-            uint64_t parts = env_u64("RT_AMD_PARTS", p.step ? 64 : 16);
+            // partitions drain faster (A/B, round 2, C2: 64 -> 5.42 ms, 32 ->
+            // 5.38, 16 -> 5.35, 8 -> 5.36; round 4, 8192 waves of 1024-thread
+            // workgroups, lean frames: 16 -> 4.453 ms, 12 -> 4.335, 10 -> 4.331,
+            // 8 -> 4.346, 4 -> +6 % on the tiles; 8-rank tile 16 -> 0.78, 8 ->
+            // 0.76 ms; C3 62.44 -> 62.37 ms).  Sliced walks keep 64 (C5: 16
+            // costs +1.6 %).
+            uint64_t parts = env_u64("RT_AMD_PARTS", p.step ? 64 : 8);
             parts = std::max<uint64_t>(1, std::min<uint64_t>({parts, kMaxParts, njobs / (16 * chunk) + 1}));
             p.nparts = (uint32_t)parts;
             HIP_TRY(hipMemsetAsync(d->counter, 0, parts * 128, s));
