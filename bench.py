@@ -122,18 +122,65 @@ def cpu_baseline(src, W, H, spp, depth, budget_s):
                                     f"({st_mt['rays']} rays, {dt_mt:.1f} s)"}}
 
 
-def main():
+def _cli_int(tok, key):
+    """The reference CLI's `key=N` argument (main.rs:23-45): `parser::starts_with`
+    on the key and on "=", then `parser::parse_int` (parser.rs:90-104): the
+    leading decimal digits as i32 (none, or an i32 overflow, is an error;
+    anything after them is ignored)."""
+    rest = tok[len(key) + 1:]
+    n = 0
+    while n < len(rest) and "0" <= rest[n] <= "9":
+        n += 1
+    if n == 0 or int(rest[:n]) > 2**31 - 1:
+        sys.exit(f"bench.py: cannot parse '{tok}' as {key}=N")
+    return rest[:n]
+
+
+def _translate_reference_args(argv):
+    """Mirror of the reference CLI's `samples=N` / `ray_depth=N` arguments
+    (raytracer/src/main.rs:23-45): rewritten to --spp / --depth."""
+    out = []
+    for tok in argv:
+        if tok.startswith("samples="):
+            out += ["--spp", _cli_int(tok, "samples")]
+        elif tok.startswith("ray_depth="):
+            out += ["--depth", _cli_int(tok, "ray_depth")]
+        else:
+            out.append(tok)
+    return out
+
+
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--config", default="c2", choices=sorted(S.CONFIGS))
+    # samples per pixel / max ray bounces of the chosen config, overridden
+    # (the reference CLI's samples= / ray_depth=, main.rs:23-45, are accepted too)
+    ap.add_argument("--spp", type=int, default=None)
+    ap.add_argument("--depth", type=int, default=None)
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--accel", default="auto", choices=["auto", "brute", "bvh"])
     ap.add_argument("--no-serial", action="store_true",
                     help="skip the RT_RNG_SERIAL (reference-identical render()) legs")
-    args = ap.parse_args()
+    args = ap.parse_args(_translate_reference_args(sys.argv[1:] if argv is None else argv))
+    if args.spp is not None and args.spp < 1:
+        sys.exit(f"bench.py: --spp must be >= 1 (got {args.spp})")
+    return args
+
+
+def workload(args):
+    """(scene maker, W, H, spp, depth) of the config, with --spp / --depth applied."""
+    make_scene, W, H, spp, depth = S.CONFIGS[args.config]
+    spp = spp if args.spp is None else args.spp
+    depth = depth if args.depth is None else args.depth
+    return make_scene, W, H, spp, depth
+
+
+def main():
+    args = parse_args()
     launched = "WORLD_SIZE" in os.environ  # torchrun: one process per GPU
     world_size = int(os.environ.get("WORLD_SIZE", "1"))
     if args.gpus < 1:
@@ -147,7 +194,7 @@ def main():
 
 
 def _setup(args):
-    make_scene, W, H, spp, depth = S.CONFIGS[args.config]
+    make_scene, W, H, spp, depth = workload(args)
     accel = {"auto": R.ACCEL_AUTO, "brute": R.ACCEL_BRUTE, "bvh": R.ACCEL_BVH}[args.accel]
     src = make_scene()
     return src, R.World(src), W, H, spp, depth, accel

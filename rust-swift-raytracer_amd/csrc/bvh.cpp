@@ -501,15 +501,18 @@ static float half_value(uint16_t h) {
     return (h & 0x8000) ? -v : v;
 }
 static uint16_t half_round(float x, bool up) {
-    static std::vector<std::pair<float, uint16_t>> table;  // every finite half, ascending
-    if (table.empty()) {
+    // every finite half, ascending; built once by a magic static (thread-safe
+    // initialisation: two worlds may load at once, the ctypes binding drops the GIL)
+    static const std::vector<std::pair<float, uint16_t>> table = [] {
+        std::vector<std::pair<float, uint16_t>> t;
         for (uint32_t h = 0; h < 65536; ++h)
-            if (((h >> 10) & 31) != 31) table.push_back({half_value((uint16_t)h), (uint16_t)h});
-        std::stable_sort(table.begin(), table.end(),
+            if (((h >> 10) & 31) != 31) t.push_back({half_value((uint16_t)h), (uint16_t)h});
+        std::stable_sort(t.begin(), t.end(),
                          [](const std::pair<float, uint16_t> &a, const std::pair<float, uint16_t> &b) {
                              return a.first < b.first;
                          });
-    }
+        return t;
+    }();
     if (up) {
         auto it = std::lower_bound(table.begin(), table.end(), x,
                                    [](const std::pair<float, uint16_t> &a, float v) { return a.first < v; });

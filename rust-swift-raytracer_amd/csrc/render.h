@@ -34,7 +34,14 @@ constexpr uint32_t kPrimaryTriStripW = 8;  // bvh.h kTriStripW
 #define RT_TRACE_RING 4
 #endif
 constexpr uint32_t kTraceRing = RT_TRACE_RING;  // chunk slots per wave (fused resolve)
-constexpr uint32_t kStatSlots = 16;        // u64 counters per wave record (TraceParams::stats)
+// u64 counters per wave record (TraceParams::stats); the -DRT_STAMPS
+// diagnostic build adds 8 fine segment stamps at slots 16..23
+#ifdef RT_STAMPS
+constexpr uint32_t kStatSlots = 24;
+#else
+constexpr uint32_t kStatSlots = 16;
+#endif
+constexpr uint32_t kStampSegs = 8;
 
 // SERIAL prediction, per pixel (built on the device from the estimate pass,
 // render.hip launch_serial_tables): P[q] = sum over pixels p < q of spp mu[p]
@@ -212,13 +219,14 @@ size_t serial_scan_scratch(uint32_t npix);
 // (TraceParams::slo) and the walks.
 // pix_spp (optional, nonzero: the pixel table pass follows): also sets ctrl[7]
 // to the iteration's stream positions per pixel (serial_pixtab_span; ctrl[7]
-// must be 0 on entry: the initial block and the finish kernel leave it so).
+// must be 0 on entry: the initial block and the finish kernel leave it so),
+// clamped to pix_emax (the pixel table's row stride).
 // counters (optional): ncounters job-queue counters (32 u32 apart) the next
 // trace pass uses, zeroed here instead of by a fill launch.
 hipError_t launch_serial_window(uint32_t *ctrl, const uint32_t *jump, uint32_t *win, uint32_t n,
                                 SerialPred M, uint32_t *lo, uint32_t L, uint32_t K, uint32_t depth,
-                                uint32_t nserial, uint32_t pix_spp, uint32_t *counters, uint32_t ncounters,
-                                hipStream_t stream);
+                                uint32_t nserial, uint32_t pix_spp, uint32_t pix_emax, uint32_t *counters,
+                                uint32_t ncounters, hipStream_t stream);
 // The pixel table pass's result (ptab: b of local pixel q at position plo(q) + e
 // = ptab[q * ctrl[7] + e]) gathered into the count table of the iteration
 // (table[jl * K + k], the layout the walks read; -1 outside the traced span)
@@ -226,7 +234,8 @@ hipError_t launch_serial_pixtab_gather(const uint32_t *ctrl, const float *ptab, 
                                        uint32_t L, uint32_t K, uint32_t spp, uint32_t nserial, hipStream_t stream);
 // the largest positions-per-pixel span an iteration can need (ptab sizing):
 // 2 (spp - 1) + 3 (depth (spp - 1) + K) + 1
-inline uint32_t serial_pixtab_emax(uint32_t spp, uint32_t K, uint32_t depth) {
+// (64-bit: the host checks it against the table's bounds before narrowing)
+inline uint64_t serial_pixtab_emax64(uint64_t spp, uint64_t K, uint64_t depth) {
     return 2u * (spp - 1u) + 3u * (depth * (spp - 1u) + K) + 1u;
 }
 // Coalescing block search (render.hip serial_coalesce_kernel): one workgroup

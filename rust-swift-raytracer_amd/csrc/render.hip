@@ -946,6 +946,12 @@ void trace_kernel(TraceParams p) {
     // iterations, iterations that walked the sphere tree, active lanes summed
     // over all iterations and over the walking ones (RT_AMD_ITER_DEBUG)
     uint32_t it_all = 0, it_walk = 0, lanes_all = 0, lanes_walk = 0;
+#ifdef RT_WALK_MIX
+    // diagnostic build only (counting variant): per sphere walk, the walk
+    // loop's iterations, those in which some lane tested a leaf, and the leaf
+    // loop's sphere trips (each the longest-active lane's view)
+    uint32_t wm_iters = 0, wm_leaf_iters = 0, wm_leaf_trips = 0, wm_walks = 0;
+#endif
 
     uint32_t pool_next = 0, pool_end = 0;  // wave-uniform job pool
     bool exhausted = false;
@@ -982,8 +988,10 @@ void trace_kernel(TraceParams p) {
     uint32_t wt_jobs_tail = 0;  // jobs claimed in the wave's last chunk
 #endif
 #ifdef RT_STAMPS
-    // diagnostic build only: wave cycles per loop segment (s_memtime deltas)
-    uint64_t stamp_acc[4] = {0, 0, 0, 0};
+    // diagnostic build only: wave cycles per loop segment (s_memtime deltas):
+    // 0 direction normalisation + loop back, 1 ray setup, 2 walks, 3 shading,
+    // 4 sample store, 5 fused resolve, 6 refill, 7 (unused)
+    uint64_t stamp_acc[kStampSegs] = {0, 0, 0, 0, 0, 0, 0, 0};
     uint64_t stamp_prev = __builtin_amdgcn_s_memtime();
 #define RT_STAMP(k)                                                       \
     do {                                                                  \
@@ -1091,13 +1099,40 @@ void trace_kernel(TraceParams p) {
                 sphere_slabs(org, inv, sph_inflation(p, bnd, best_t), nlo, nhi);
                 const uint32_t octm = ((oct & 1u) ? 48u : 0u) | ((oct & 2u) ? 48u << 8 : 0u) |
                                       ((oct & 4u) ? 48u << 16 : 0u);
+#ifdef RT_WALK_MIX
+                uint32_t wi = 0, wl = 0, wt = 0;
+#endif
                 do {
                     uint32_t leaf;
-                    if (sphere_node<kLds>(view, inv, oct, octm, best_t, nlo, nhi, node, leaf,
-                                          node_tests))
+                    const bool lf = sphere_node<kLds>(view, inv, oct, octm, best_t, nlo, nhi, node, leaf,
+                                                      node_tests);
+#ifdef RT_WALK_MIX
+                    if (kCount) {
+                        ++wi;
+                        const bool any1 = __ballot(lf) != 0;
+                        const bool any2 = __ballot(lf && (leaf & 7u) >= 2u) != 0;
+                        wl += any1 ? 1u : 0u;
+                        wt += any2 ? 2u : any1 ? 1u : 0u;
+                    }
+#endif
+                    if (lf)
                         sphere_leaf(p, view, org, dir, inv, leaf, best_t, best_i, bnd, nlo, nhi,
                                     sph_tests);
                 } while (node != kEnd && (!kStep || --budget != 0));
+#ifdef RT_WALK_MIX
+                if (kCount) {
+                    // (wave maxima over the walking lanes: the longest-active lane saw every iteration)
+                    for (uint32_t off = 1; off < kWave; off <<= 1) {
+                        wi = max(wi, (uint32_t)__shfl_xor((int)wi, (int)off));
+                        wl = max(wl, (uint32_t)__shfl_xor((int)wl, (int)off));
+                        wt = max(wt, (uint32_t)__shfl_xor((int)wt, (int)off));
+                    }
+                    wm_iters += wi;
+                    wm_leaf_iters += wl;
+                    wm_leaf_trips += wt;
+                    wm_walks += 1u;
+                }
+#endif
                 if (node == kEnd) phase = kTriInit;
             }
             if (phase == kTriInit) {
@@ -1343,6 +1378,7 @@ void trace_kernel(TraceParams p) {
                 active = false;
             }
         }
+        RT_STAMP(4);
         if (kCount && nact != 0) {  // (wave-uniform: every lane counts the same)
             const bool wk = __ballot(walked) != 0;
             ++it_all;
@@ -1378,6 +1414,7 @@ void trace_kernel(TraceParams p) {
                 if (fin) slot = ~0u;
             }
         }
+        RT_STAMP(5);
         // ---- refill lanes whose path ended (active-ray compaction) -------
         // (with the fused resolve a new chunk needs a free ring slot: with all
         // kTraceRing slots waiting on unfinished samples the lanes stay idle)
@@ -1490,6 +1527,7 @@ void trace_kernel(TraceParams p) {
                 prefetch_pending = true;
             }
         }
+        RT_STAMP(6);
         if (renorm) dir = unit(vdir);
         RT_STAMP(0);
         if (__ballot(active) == 0 && exhausted) break;
@@ -1510,8 +1548,14 @@ void trace_kernel(TraceParams p) {
 #pragma unroll
         for (int k = 0; k < 6; ++k) w[k < 4 ? k : k + 4] += c[k];
         for (int k = 0; k < 4; ++k) w[10 + k] += mix[k];
+#ifdef RT_WALK_MIX
+        w[4] += wm_iters; w[5] += wm_leaf_iters; w[6] += wm_leaf_trips; w[7] += wm_walks;
+#endif
 #ifdef RT_STAMPS
-        for (int k = 0; k < 4; ++k) w[4 + k] += stamp_acc[k];
+        // coarse shares (stamp_cycles): refill + store + resolve + loop, setup, walks, shade
+        w[4] += stamp_acc[0] + stamp_acc[4] + stamp_acc[5] + stamp_acc[6];
+        for (int k = 1; k < 4; ++k) w[4 + k] += stamp_acc[k];
+        for (uint32_t k = 0; k < kStampSegs; ++k) w[16 + k] += stamp_acc[k];
 #endif
 #ifdef RT_WAVE_TIMES
         w[4] = wt_start;
@@ -1724,7 +1768,7 @@ __global__ __launch_bounds__(256) void serial_window_kernel(uint32_t *__restrict
                                                             uint32_t *__restrict__ win, uint32_t n,
                                                             SerialPred M, uint32_t *__restrict__ lo,
                                                             uint32_t L, uint32_t Kmax, uint32_t depth,
-                                                            uint32_t nserial, uint32_t pix_spp,
+                                                            uint32_t nserial, uint32_t pix_spp, uint32_t pix_emax,
                                                             uint32_t *__restrict__ counters, uint32_t ncounters) {
     if (ctrl[0] != 0u) return;
     // the following trace pass's job counters (instead of a fill launch)
@@ -1750,6 +1794,9 @@ __global__ __launch_bounds__(256) void serial_window_kernel(uint32_t *__restrict
                 const uint32_t hi = 2u * jz + 3u * (lz + K - 1u), lo0 = 2u * jf + 3u * lf;
                 span = max(span, hi >= lo0 ? hi - lo0 + 1u : 1u);
             }
+            // (clamped to the table's row stride: every reader takes ctrl[7] as
+            // is, and a position past it reads as "left the window")
+            span = min(span, pix_emax);
             if (span) atomicMax(ctrl + 7, span);
         }
     }
@@ -2578,12 +2625,13 @@ hipError_t launch_serial_tables(double *tab, double *scratch, uint32_t npix, uin
 
 hipError_t launch_serial_window(uint32_t *ctrl, const uint32_t *jump, uint32_t *win, uint32_t n,
                                 SerialPred M, uint32_t *lo, uint32_t L, uint32_t K, uint32_t depth,
-                                uint32_t nserial, uint32_t pix_spp, uint32_t *counters, uint32_t ncounters,
-                                hipStream_t stream) {
+                                uint32_t nserial, uint32_t pix_spp, uint32_t pix_emax, uint32_t *counters,
+                                uint32_t ncounters, hipStream_t stream) {
     if (!n) return hipSuccess;
     const uint32_t threads = std::max((n + kWinPerThread - 1) / kWinPerThread, lo ? std::min(L, 1u << 16) : 0u);
     hipLaunchKernelGGL(serial_window_kernel, dim3((threads + 255) / 256), dim3(256), 0, stream, ctrl,
-                       jump, win, n, M, lo, L, K, depth, nserial, pix_spp, counters, counters ? ncounters : 0u);
+                       jump, win, n, M, lo, L, K, depth, nserial, pix_spp, pix_emax, counters,
+                       counters ? ncounters : 0u);
     return hipGetLastError();
 }
 

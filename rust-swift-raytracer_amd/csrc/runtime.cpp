@@ -115,18 +115,25 @@ static int device_for(WorldState &w, int want, DeviceState *&out) {
         // (RT_AMD_TRI_WIDE=0: the binary walk)
         const TriangleBVH &tw = w.tbvh;
         const uint32_t tw_depth = std::max<uint32_t>(1u, 3u * tw.wdepth);
-        const bool wide = !tw.wnodes.empty() && env_u64("RT_AMD_TRI_WIDE", 1) != 0 &&
-                          (size_t)tw_depth * trace_block_threads(true, 3, 0) * 2u <= 64u * 1024u;
-        const int tri = wide ? 3 : trace_mesh_kind(w.packed.ntri > 0, !w.tbvh.nodes.empty());
+        bool wide = !tw.wnodes.empty() && env_u64("RT_AMD_TRI_WIDE", 1) != 0 &&
+                    (size_t)tw_depth * trace_block_threads(true, 3, 0) * 2u <= 64u * 1024u;
+        int tri = wide ? 3 : trace_mesh_kind(w.packed.ntri > 0, !w.tbvh.nodes.empty());
         // the stack's LDS (kinds 0 and 1: SERIAL passes keep the binary walk)
         auto stack_lds = [&](int c, uint32_t threads) -> size_t {
             return tri == 3 && c != 2 ? (size_t)tw_depth * threads * 2u : 0u;
         };
-        for (int c = 0; c < 3; ++c)
-            for (int st = 0; st < 2; ++st) {
-                HIP_TRY(trace_occupancy(&d->blocks_per_cu[c][st], 0, stack_lds(c, 256), st, tri, c));
-                HIP_TRY(trace_occupancy(&d->blocks_per_cu_bvh[c][st], 1, stack_lds(c, 256), st, tri, c));
-            }
+        // workgroups per CU of the kernels without the LDS sphere tree
+        auto occupancy_global = [&]() -> hipError_t {
+            for (int c = 0; c < 3; ++c)
+                for (int st = 0; st < 2; ++st) {
+                    hipError_t e = trace_occupancy(&d->blocks_per_cu[c][st], 0, stack_lds(c, 256), st, tri, c);
+                    if (e == hipSuccess)
+                        e = trace_occupancy(&d->blocks_per_cu_bvh[c][st], 1, stack_lds(c, 256), st, tri, c);
+                    if (e != hipSuccess) return e;
+                }
+            return hipSuccess;
+        };
+        HIP_TRY(occupancy_global());
         // scene upload (once per device)
         const PackedScene &p = w.packed;
         auto up = [&](void **dst, const std::vector<float> &src) -> hipError_t {
@@ -176,15 +183,32 @@ static int device_for(WorldState &w, int want, DeviceState *&out) {
                     m16[i] = bv.miss[i] == kNodeEnd ? (uint16_t)0xFFFF : (uint16_t)bv.miss[i];
                 HIP_TRY(hipMalloc((void **)&d->bvh_miss16, m16.size() * 2));
                 HIP_TRY(hipMemcpy(d->bvh_miss16, m16.data(), m16.size() * 2, hipMemcpyHostToDevice));
-                bool fits = true;
-                for (int c = 0; c < 3; ++c)
-                    for (int st = 0; st < 2; ++st) {
-                        const uint32_t lt = trace_block_threads(true, tri == 3 && c == 2 ? 2 : tri, c);
-                        const size_t sb = stack_lds(c, lt);
-                        HIP_TRY(trace_occupancy(&d->blocks_per_cu_lds[c][st], 2,
-                                                sb ? ((lds + 15u) & ~(size_t)15u) + sb : lds, st, tri, c));
-                        fits = fits && d->blocks_per_cu_lds[c][st] > 0;
-                    }
+                // every kernel kind must fit its LDS (the tree, plus the wide
+                // walk's stacks for the frame kinds); when the stacks are what
+                // does not fit, the frames take the binary triangle walk and
+                // every kind keeps the LDS sphere tree
+                auto occupancy_lds = [&](bool &fits) -> hipError_t {
+                    fits = true;
+                    for (int c = 0; c < 3; ++c)
+                        for (int st = 0; st < 2; ++st) {
+                            const uint32_t lt = trace_block_threads(true, tri == 3 && c == 2 ? 2 : tri, c);
+                            const size_t sb = stack_lds(c, lt);
+                            const hipError_t e = trace_occupancy(&d->blocks_per_cu_lds[c][st], 2,
+                                                                 sb ? ((lds + 15u) & ~(size_t)15u) + sb : lds, st,
+                                                                 tri, c);
+                            if (e != hipSuccess) return e;
+                            fits = fits && d->blocks_per_cu_lds[c][st] > 0;
+                        }
+                    return hipSuccess;
+                };
+                bool fits = false;
+                HIP_TRY(occupancy_lds(fits));
+                if (!fits && wide) {
+                    wide = false;
+                    tri = trace_mesh_kind(w.packed.ntri > 0, !w.tbvh.nodes.empty());
+                    HIP_TRY(occupancy_global());
+                    HIP_TRY(occupancy_lds(fits));
+                }
                 if (fits) d->lds_bytes = lds;
             }
         }
@@ -781,7 +805,21 @@ int render_frame(WorldState &w, const CameraModel &cam, size_t width, size_t hei
         stats->bvh_node_tests = st[3];
         stats->big_sphere_tests = use_bvh ? st[0] * (uint64_t)d->nbig : st[0] * (uint64_t)d->nsph;
         for (int k = 0; k < 4; ++k) stats->stamp_cycles[k] = st[4 + k];
+#ifdef RT_STAMPS
+        {   // fine segments (tools/stamps.py parses this line)
+            double tot = 0;
+            for (uint32_t k = 0; k < kStampSegs; ++k) tot += (double)st[16 + k];
+            std::fprintf(stderr, "stamp segments:");
+            for (uint32_t k = 0; k < kStampSegs; ++k) std::fprintf(stderr, " %.4f", st[16 + k] / std::max(1.0, tot));
+            std::fprintf(stderr, " cycles %.6e\n", tot);
+        }
+#endif
         stats->tri_node_tests = st[8];
+#ifdef RT_WALK_MIX
+        std::fprintf(stderr, "walk mix: %llu walks, %.2f iterations per walk, %.2f with a leaf, %.2f leaf trips\n",
+                     st[7], st[4] / std::max(1.0, (double)st[7]), st[5] / std::max(1.0, (double)st[7]),
+                     st[6] / std::max(1.0, (double)st[7]));
+#endif
         if (env_u64("RT_AMD_ITER_DEBUG", 0))
             std::fprintf(stderr, "iteration mix: %llu iterations (%.1f active lanes), %llu walking (%.1f lanes), "
                          "%llu other (%.1f lanes)\n", st[10], st[12] / std::max(1.0, (double)st[10]), st[11],
@@ -916,7 +954,7 @@ static int serial_find_states(WorldState &w, const CameraModel &cam, size_t widt
         // instead of the count pass's L K, and independent ones, unlike the
         // coalescing search's chains.  RT_AMD_SERIAL_PIXTAB=0: the searches below.
         bool pixtab = spp >= 4 && env_u64("RT_AMD_SERIAL_PIXTAB", 1) != 0;
-        bool coalesce = !pixtab && env_u64("RT_AMD_SERIAL_COALESCE", trees ? 0 : 1) != 0 && depth < 1024;
+        bool coalesce = false;
         // (iterations of 128 k samples in blocks of 32 for the coalescing search,
         // profiles/round3_serial/coalesce_sweep*.log; 16 k for the count pass;
         // the pixel table: 32 k at 16 spp, x sqrt(spp / 16) in powers of two --
@@ -924,17 +962,24 @@ static int serial_find_states(WorldState &w, const CameraModel &cam, size_t widt
         // per iteration as 1 / L; profiles/round4_serial/pixtab_sweep*.log:
         // world.txt 960x540x16 16 k / 32 k / 64 k -> 141 / 114 / 121 ms, RTOW
         // 1920x1080x64 64 k / 128 k / 256 k -> 1.01 / 1.07 / 1.24 s)
-        uint64_t Ldef = coalesce ? 131072 : 16384;
-        if (pixtab) {
-            Ldef = 32768;
-            for (uint64_t q = 64; q <= spp; q *= 4) Ldef *= 2;        // 64 spp: 64 k, 256 spp: 128 k
-            for (uint64_t q = spp; q < 16 && Ldef > 8192; q *= 4) Ldef /= 2;  // 4 spp: 16 k
-        }
-        const uint64_t L = std::max<uint64_t>(1, std::min<uint64_t>(env_u64("RT_AMD_SERIAL_CHUNK", Ldef), N));
-        // windows are sized for the deviation over Lw samples (default L; a
-        // longer Lw widens them, a shorter iteration stops less often)
-        const uint64_t Lw = std::max<uint64_t>(1, env_u64("RT_AMD_SERIAL_WLEN", L));
-        const uint64_t n0 = std::min(N, Lw);
+        uint64_t L = 1, Lw = 1, n0 = 1;
+        // the iteration length for the search chosen (planned again, without the
+        // pixel table, when its table turns out too large below)
+        auto plan = [&]() {
+            coalesce = !pixtab && env_u64("RT_AMD_SERIAL_COALESCE", trees ? 0 : 1) != 0 && depth < 1024;
+            uint64_t Ldef = coalesce ? 131072 : 16384;
+            if (pixtab) {
+                Ldef = 32768;
+                for (uint64_t q = 64; q <= spp; q *= 4) Ldef *= 2;        // 64 spp: 64 k, 256 spp: 128 k
+                for (uint64_t q = spp; q < 16 && Ldef > 8192; q *= 4) Ldef /= 2;  // 4 spp: 16 k
+            }
+            L = std::max<uint64_t>(1, std::min<uint64_t>(env_u64("RT_AMD_SERIAL_CHUNK", Ldef), N));
+            // windows are sized for the deviation over Lw samples (default L; a
+            // longer Lw widens them, a shorter iteration stops less often)
+            Lw = std::max<uint64_t>(1, env_u64("RT_AMD_SERIAL_WLEN", L));
+            n0 = std::min(N, Lw);
+        };
+        plan();
         HIP_TRY(grow(d->stab, d->stab_cap, serial_tab_doubles((uint32_t)npix)));
         HIP_TRY(grow(d->sscan, d->sscan_cap, serial_scan_scratch((uint32_t)npix)));
         double *const sums = d->stab + 5 * npix + 2;  // {sum ss, dmax, V(n0), lost count}
@@ -952,51 +997,61 @@ static int serial_find_states(WorldState &w, const CameraModel &cam, size_t widt
                                               1.0 + 1.0 / per, d->stab, (uint32_t)npix, s));
             }
         }
-        HIP_TRY(launch_serial_tables(d->stab, d->sscan, (uint32_t)npix, (uint32_t)spp, (uint32_t)L, (uint32_t)n0, s));
-        HIP_TRY(hipEventRecord(d->sev[2], s));
-        double sm[4];
-        HIP_TRY(hipMemcpyAsync(sm, sums, sizeof(sm), hipMemcpyDeviceToHost, s));
-        HIP_TRY(hipStreamSynchronize(s));
-        if (sm[3] != 0.0) {
-            set_error("RT_RNG_SERIAL: estimate pass lost a sample's draw count");
-            return -5;
-        }
-        double dmax = 0.0;  // largest predicted offset within L + L/4 samples: the window
-        {
-            uint64_t bits;
-            std::memcpy(&bits, &sm[1], 8);
-            std::memcpy(&dmax, &bits, 8);
-        }
-        const double sigma = std::sqrt(std::max(sm[0], 0.0) / (double)(N * R)) + 0.05;
         const SerialPred pred{d->stab, d->stab + npix + 1, (uint32_t)spp, (uint32_t)npix};
-        // 2. iterations of L samples from the first unresolved one (ctrl[4]),
-        // K candidates per sample, spanning +-z sigma of the deviation of the
-        // true offset from the predicted one at the end of L samples.  Narrow
-        // windows trade progress for work: an iteration resolves samples up
-        // to where the path leaves a window, and the next one starts there
-        // with its windows re-centred (no host round trip).
-        // (tools/serial_sweep.sh on the c_raytracer, C1 and RTOW frames: L 2048
-        // -> 103 / 9 / 126 ms, 4096 -> 71 / 7 / 85, 16384 -> 56 / 6 / 61, 65536 ->
-        // 72 / 6 / 64; z 1.0 / 1.5 / 2.0 within 5 %: short iterations pay the
-        // launch tail, long ones the sqrt(L) wider windows)
         const double z = (double)env_u64("RT_AMD_SERIAL_Z10", 15) / 10.0;
-        const double spread = std::sqrt((double)Lw * (1.0 + 1.0 / (double)(spp * R)));
-        uint64_t K = (uint64_t)std::ceil(2.0 * z * sigma * spread) + 2 * (uint64_t)depth + 2;
-        if (const uint64_t k = env_u64("RT_AMD_SERIAL_K", 0)) K = k;  // (tests: narrow windows)
-        // sample a + 1's window must hold every b of sample a: K >= 2 depth + 2
-        K = std::min<uint64_t>(std::max<uint64_t>(K, 2 * (uint64_t)depth + 2), (uint64_t)depth * L + 1);
-        if (L * K > 0x7FFFFFFFull) {
-            set_error("RT_RNG_SERIAL: candidate table too large");
-            return -5;
+        double dmax = 0.0;  // largest predicted offset within L + L/4 samples: the window
+        uint64_t K = 0, npq_max = 0, emax = 0;
+        double sm[4] = {0.0, 0.0, 0.0, 0.0};  // {sum ss, dmax bits, V(n0), lost-count flag}
+        double sigma = 0.0;
+        for (;;) {
+            HIP_TRY(launch_serial_tables(d->stab, d->sscan, (uint32_t)npix, (uint32_t)spp, (uint32_t)L,
+                                         (uint32_t)n0, s));
+            HIP_TRY(hipEventRecord(d->sev[2], s));
+            HIP_TRY(hipMemcpyAsync(sm, sums, sizeof(sm), hipMemcpyDeviceToHost, s));
+            HIP_TRY(hipStreamSynchronize(s));
+            if (sm[3] != 0.0) {
+                set_error("RT_RNG_SERIAL: estimate pass lost a sample's draw count");
+                return -5;
+            }
+            {
+                uint64_t bits;
+                std::memcpy(&bits, &sm[1], 8);
+                std::memcpy(&dmax, &bits, 8);
+            }
+            sigma = std::sqrt(std::max(sm[0], 0.0) / (double)(N * R)) + 0.05;
+            // 2. iterations of L samples from the first unresolved one (ctrl[4]),
+            // K candidates per sample, spanning +-z sigma of the deviation of the
+            // true offset from the predicted one at the end of L samples.  Narrow
+            // windows trade progress for work: an iteration resolves samples up
+            // to where the path leaves a window, and the next one starts there
+            // with its windows re-centred (no host round trip).
+            // (tools/serial_sweep.sh on the c_raytracer, C1 and RTOW frames: L 2048
+            // -> 103 / 9 / 126 ms, 4096 -> 71 / 7 / 85, 16384 -> 56 / 6 / 61, 65536 ->
+            // 72 / 6 / 64; z 1.0 / 1.5 / 2.0 within 5 %: short iterations pay the
+            // launch tail, long ones the sqrt(L) wider windows)
+            const double spread = std::sqrt((double)Lw * (1.0 + 1.0 / (double)(spp * R)));
+            K = (uint64_t)std::ceil(2.0 * z * sigma * spread) + 2 * (uint64_t)depth + 2;
+            if (const uint64_t k = env_u64("RT_AMD_SERIAL_K", 0)) K = k;  // (tests: narrow windows)
+            // sample a + 1's window must hold every b of sample a: K >= 2 depth + 2
+            K = std::min<uint64_t>(std::max<uint64_t>(K, 2 * (uint64_t)depth + 2), (uint64_t)depth * L + 1);
+            if (L * K > 0x7FFFFFFFull) {
+                set_error("RT_RNG_SERIAL: candidate table too large");
+                return -5;
+            }
+            // (the coalescing workgroup keeps K candidates' u16 slots and K + depth
+            // + 1 live offsets in LDS, <= 64 KB: wider windows take the count pass)
+            if (K > 4096 || serial_coalesce_search_lds((uint32_t)K, depth) > 64 * 1024) coalesce = false;
+            // the pixel table's bounds (64-bit: no wrap before the checks): pixels an
+            // iteration touches x the widest span of positions one pixel's windows cover
+            npq_max = L / spp + 2;
+            emax = pixtab ? serial_pixtab_emax64(spp, K, depth) : 0;
+            if (!pixtab || (npq_max * emax <= (1ull << 28) && emax <= 0x7FFFFFFFull)) break;
+            // too large: plan the iterations as without the pixel table (L, and
+            // with it K and the reach; the coalescing search where the rule picks it)
+            pixtab = false;
+            plan();
+            HIP_TRY(hipMemsetAsync(sums + 1, 0, sizeof(double), s));  // (the reach: atomicMax)
         }
-        // (the coalescing workgroup keeps K candidates' u16 slots and K + depth
-        // + 1 live offsets in LDS, <= 64 KB: wider windows take the count pass)
-        if (K > 4096 || serial_coalesce_search_lds((uint32_t)K, depth) > 64 * 1024) coalesce = false;
-        // the pixel table's bounds: pixels an iteration touches x the widest
-        // span of positions one pixel's windows can cover
-        const uint64_t npq_max = L / spp + 2;
-        const uint64_t emax = pixtab ? serial_pixtab_emax((uint32_t)spp, (uint32_t)K, depth) : 0;
-        if (pixtab && (npq_max * emax > (1ull << 28) || emax > 0x7FFFFFFFull)) pixtab = false;
         // the block walks read the pixel table directly (RT_AMD_SERIAL_PGATHER=1:
         // through a gathered L x K count table instead, the first build: 27 us per
         // iteration more at 32 k x 617)
@@ -1078,8 +1133,8 @@ static int serial_find_states(WorldState &w, const CameraModel &cam, size_t widt
                 // (the pixel table pass's job counters are zeroed by the window kernel)
                 HIP_TRY(launch_serial_window(d->sctrl, d->sjump, d->swin, (uint32_t)wlen, pred, d->slo,
                                              (uint32_t)L, (uint32_t)K, depth, (uint32_t)N,
-                                             pixtab ? (uint32_t)spp : 0u, pixtab ? d->counter : nullptr,
-                                             kPixtabParts, s));
+                                             pixtab ? (uint32_t)spp : 0u, (uint32_t)emax,
+                                             pixtab ? d->counter : nullptr, kPixtabParts, s));
                 if (pixtab) {
                     SerialPass sp{kRngSerialPixel, 0u, (uint32_t)npq_max, (uint32_t)emax, d->swin, pred, d->sctrl,
                                   d->slo};

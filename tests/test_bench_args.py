@@ -42,3 +42,37 @@ def test_more_gpus_than_visible_is_refused():
 def test_gpus_must_be_positive():
     r = _run(["--gpus", "0"], {})
     assert r.returncode != 0 and "--gpus must be >= 1" in r.stderr
+
+
+def _bench_module():
+    import importlib.util
+
+    spec = importlib.util.spec_from_file_location("bench_under_test", BENCH)
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def test_spp_and_depth_override_the_config():
+    """--spp / --depth (and the reference CLI's samples= / ray_depth=,
+    main.rs:23-45) replace the config's spp and depth; the defaults keep the
+    config's, so the driver's bench line is unchanged."""
+    b = _bench_module()
+    _, W, H, spp, depth = b.workload(b.parse_args([]))
+    assert (W, H, spp, depth) == (1920, 1080, 64, 8)
+    _, W, H, spp, depth = b.workload(b.parse_args(["--spp", "16", "--depth", "4"]))
+    assert (W, H, spp, depth) == (1920, 1080, 16, 4)
+    _, _, _, spp, depth = b.workload(b.parse_args(["--config", "c3", "--depth", "5"]))
+    assert (spp, depth) == (256, 5)
+    # the reference's argument syntax: leading digits only (parser.rs:90-104)
+    _, _, _, spp, depth = b.workload(b.parse_args(["samples=32", "ray_depth=3x"]))
+    assert (spp, depth) == (32, 3)
+
+
+def test_bad_spp_and_reference_args_are_refused():
+    r = _run(["--spp", "0"], {})
+    assert r.returncode != 0 and "--spp must be >= 1" in r.stderr
+    r = _run(["samples=abc"], {})
+    assert r.returncode != 0 and "cannot parse 'samples=abc'" in r.stderr
+    r = _run(["ray_depth=99999999999"], {})
+    assert r.returncode != 0 and "cannot parse" in r.stderr
