@@ -305,8 +305,10 @@ inline int trace_mesh_kind(bool triangles, bool tree) { return !triangles ? 0 : 
 size_t trace_lds_bytes(const TraceParams &p);
 // the sphere tree's LDS copy (render.hip stage_tree)
 __host__ __device__ inline size_t trace_tree_lds(uint32_t nnodes, uint32_t nprims, uint32_t nsph_padded) {
-    return (size_t)nnodes * 48 + (size_t)nprims * 20 + (size_t)nsph_padded * 36;
+    return (size_t)nnodes * 64 + (size_t)nprims * 20 + (size_t)nsph_padded * 36;
 }
+// the LDS copy addresses its 64-B node records with u16 byte addresses (0xFFFF: end)
+constexpr uint32_t kLdsTreeMaxNodes = 1023;
 // threads per trace workgroup: LDS-tree kernels (per kernel family, trace_mesh_kind
 // or 3 for the wide walk) vs global
 uint32_t trace_block_threads(bool lds, int mesh, int kind);

@@ -194,7 +194,14 @@ __device__ __forceinline__ bool sphere_candidate(float4 S, F3 org, F3 dir, int i
     const bool v1 = tmin < r1;
     const float c = v1 ? r1 : r2;
     const bool valid = v1 || (tmin < r2);
-    const bool take = valid && (c < best_t || (c == best_t && best_t < __builtin_inff() && idx < best_i));
+    // c < best_t || (c == best_t && best_t < inf && idx < best_i) as one
+    // unsigned compare of (t bits, index) keys: both t are positive (c > t_min,
+    // best_t > t_min or +inf), so their bits order like the values; best_i is
+    // -1 (all ones) only while best_t is +inf, and c = +inf, which that rule
+    // never takes, is excluded
+    const uint64_t kc = ((uint64_t)__float_as_uint(c) << 32) | (uint32_t)idx;
+    const uint64_t kb = ((uint64_t)__float_as_uint(best_t) << 32) | (uint32_t)best_i;
+    const bool take = valid && c != __builtin_inff() && kc < kb;
     if (take) { best_t = c; best_i = idx; }
     return take;
 }
@@ -204,7 +211,7 @@ constexpr float kErrK = 3.0e-3f;  // >= 2.7x the derived sqrt(30u) = 1.12e-3 (DE
 // Where the traversal reads the tree from: global memory (any size) or the
 // workgroup's LDS copy (staged once per persistent workgroup).
 struct BvhView {
-    const float4 *nodes;     // global: 2 per node; LDS: 48-B records (box | 8 x u16 links)
+    const float4 *nodes;     // global: 2 per node; LDS: 64-B records (box | 8 x u32 link pairs)
     const uint32_t *miss32;  // global: 8 x u32 per node
     const uint16_t *miss16;  // (unused: the LDS links live in the node records)
     const float4 *prims;
@@ -256,16 +263,18 @@ __device__ __forceinline__ void spheres_big(const TraceParams &p, F3 org, F3 dir
 // ray enters is handed back in `leaf` as (first << 3) | count for
 // sphere_leaf.  (Deferring leaf tests until every lane of the wave has one
 // pending -- "while-while" -- measured 6% slower on C2 and 60% on C5.)
+// kLds: `ooff` = 4 * octant (the link word's offset in the record); global
+// memory: `ooff` = the octant, `octm` unused.
 template <bool kLds>
-__device__ __forceinline__ bool sphere_node(const BvhView &v, F3 inv, uint32_t oct, uint32_t octm,
-                                            float best_t, F3 nlo, F3 nhi, uint32_t &node,
-                                            uint32_t &leaf, uint32_t &node_tests) {
+__device__ __forceinline__ bool sphere_node(const BvhView &v, F3 inv, uint32_t ooff, float best_t, F3 nlo,
+                                            F3 nhi, uint32_t &node, uint32_t &leaf, uint32_t &node_tests) {
     ++node_tests;
-    // LDS copy: `node` is the record's LDS byte address (48-B records: box | 8
-    // u16 links; links and child words are staged as addresses), so the box
-    // needs no address arithmetic and the link one add
+    // LDS copy: `node` is the record's LDS byte address (64-B records: box |
+    // per octant one u32 of two u16 links: the node to visit next when the box
+    // is entered -- the near child, or for a leaf its miss link -- and when it
+    // is skipped), so the next node is one select of a half of one LDS word
     float4 B0, B1;
-    uint32_t miss;
+    uint32_t miss, hit = 0;
     if (kLds) {
 #if defined(__HIP_DEVICE_COMPILE__)
         // `node` is the record's LDS address (staged as such: no base add)
@@ -273,7 +282,9 @@ __device__ __forceinline__ bool sphere_node(const BvhView &v, F3 inv, uint32_t o
         const lds_cptr rec = (lds_cptr)(uintptr_t)node;
         B0 = *(const __attribute__((address_space(3))) float4 *)rec;
         B1 = *(const __attribute__((address_space(3))) float4 *)(rec + 16);
-        miss = *(const __attribute__((address_space(3))) uint16_t *)(rec + 32 + 2 * oct);
+        const uint32_t lw = *(const __attribute__((address_space(3))) uint32_t *)(rec + 32 + ooff);
+        hit = lw & 0xFFFFu;
+        miss = lw >> 16;
 #else
         B0 = B1 = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
         miss = 0;
@@ -281,7 +292,7 @@ __device__ __forceinline__ bool sphere_node(const BvhView &v, F3 inv, uint32_t o
     } else {
         B0 = v.nodes[2 * node];
         B1 = v.nodes[2 * node + 1];
-        miss = v.miss32[8 * node + oct];
+        miss = v.miss32[8 * node + ooff];
     }
     // Slab values b * inv - lo * inv as one fma each, nlo = -(lo * inv) per ray
     // (sphere_slabs): the result is the exact slab value of a face moved by
@@ -302,13 +313,16 @@ __device__ __forceinline__ bool sphere_node(const BvhView &v, F3 inv, uint32_t o
     // compiler folds it into tn > min(tf, best_t) and canonicalises best_t at
     // every node.)
     const bool skip = tn > tf || tf < 0.001f || __float_as_int(tn) > __float_as_int(best_t);
+    if (kLds) {
+        // staged leaf word: (first << 3) | count for a leaf (count >= 1), 0 else
+        leaf = __float_as_uint(B0.w);
+        node = skip ? miss : hit;
+        return !skip && leaf != 0u;
+    }
     const uint32_t a = __float_as_uint(B0.w);
     const bool is_leaf = (a & kLeafBitDev) != 0;
-    // near child first: with kLds the staged axis word is 8 * axis and octm
-    // holds 48 * (octant bit) per axis in bytes 0..2, so the right child's
-    // record (+48) is one bit-field extract away
-    const uint32_t child = kLds ? a + __builtin_amdgcn_ubfe(octm, __float_as_uint(B1.w), 8)
-                                : a + ((oct >> __float_as_uint(B1.w)) & 1u);
+    // near child first
+    const uint32_t child = a + ((ooff >> __float_as_uint(B1.w)) & 1u);
     node = (skip || is_leaf) ? miss : child;
     // (returned as a flag, so the caller branches on it directly; leaf is only
     // read when it is set)
@@ -323,17 +337,17 @@ __device__ __forceinline__ void sphere_slabs(F3 org, F3 inv, float e, F3 &nlo, F
     nhi = f3(-((org.x - e) * inv.x), -((org.y - e) * inv.y), -((org.z - e) * inv.z));
 }
 
-// Tests a pending leaf; on a new best, re-derives the inflated origin box.
-__device__ __forceinline__ void sphere_leaf(const TraceParams &p, const BvhView &v, F3 org, F3 dir,
-                                            F3 inv, uint32_t leaf, float &best_t, int &best_i,
-                                            SphBound bnd, F3 &nlo, F3 &nhi, uint32_t &sph_tests) {
+// Tests a pending leaf.  The node boxes keep the inflation derived from the
+// best t at the walk's start: a larger best t only inflates them more (still
+// exact), and re-deriving it after every new best (the round-1
+// to round-4 code) cost ~20 VALU per improvement for boxes ~1 % tighter.
+__device__ __forceinline__ void sphere_leaf(const BvhView &v, F3 org, F3 dir, uint32_t leaf, float &best_t,
+                                            int &best_i, uint32_t &sph_tests) {
     const uint32_t first = leaf >> 3, end = first + (leaf & 7u);
-    bool changed = false;
     for (uint32_t j = first; j < end; ++j) {
         ++sph_tests;
-        changed |= sphere_candidate(v.prims[j], org, dir, (int)v.ids[j], best_t, best_i);
+        sphere_candidate(v.prims[j], org, dir, (int)v.ids[j], best_t, best_i);
     }
-    if (changed) sphere_slabs(org, inv, sph_inflation(p, bnd, best_t), nlo, nhi);
 }
 
 // ------------------------------------------------------------ triangle stage
@@ -738,12 +752,17 @@ __device__ __forceinline__ void resolve_chunk(const TraceParams &p, const float 
 
 // The sphere tree's view for a kernel; kLds: copied into the workgroup's LDS
 // (one barrier).  Returns the walk's first node (its LDS address with kLds).
-// LDS layout: node records (48 B: box float4 x 2 | 8 x u16 links) | prims
+// LDS layout: node records (64 B: box float4 x 2 | 8 x u32 links) | prims
 // (float4) | shade (2 x float4 / sphere) | ids (u32) | kinds (u32), at the
-// start of the dynamic LDS (trace_lds_bytes).  Node references become record
-// LDS addresses (base + index * 48; the kernels have no static LDS before it,
-// so base is 0 and they stay below 65520: the copy holds < 1366 nodes); 0xFFFF
-// stays the end marker.
+// start of the dynamic LDS (trace_lds_bytes).  A record is
+//   (lo.xyz, leaf word) (hi.xyz, 0) and, per ray octant o, the u32
+//   next(o) | miss(o) << 16: the node to visit when the box is entered (the
+//   near child along the split axis for the octant's sign, the DFS order of
+//   bvh.h; a leaf's own miss link) and when it is skipped,
+// with the leaf word (first << 3) | count for leaves and 0 for inner nodes.
+// Node references are record LDS addresses (base + index * 64; the kernels
+// have no static LDS before it, so base is 0 and they stay below 0xFFFF: the
+// copy holds <= kLdsTreeMaxNodes nodes); 0xFFFF stays the end marker.
 template <bool kLds>
 __device__ __forceinline__ uint32_t stage_tree(const TraceParams &p, float4 *lds, BvhView &view) {
     if (!kLds) {
@@ -753,29 +772,32 @@ __device__ __forceinline__ uint32_t stage_tree(const TraceParams &p, float4 *lds
     }
     float4 *n4 = lds;
     const uint32_t lbase = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) float4 *)lds;
-    float4 *p4 = n4 + 3 * p.nnodes;
+    float4 *p4 = n4 + 4 * p.nnodes;
     float4 *s4 = p4 + p.nprims;
     uint32_t *id = reinterpret_cast<uint32_t *>(s4 + 2 * p.nsph_padded);
     uint32_t *kd = id + p.nprims;
     const uint16_t *g16 = p.bvh_miss16;
+    auto addr = [&](uint32_t l) { return l == 0xFFFFu ? 0xFFFFu : lbase + l * 64u; };
     for (uint32_t i = threadIdx.x; i < p.nnodes; i += blockDim.x) {
         float4 b0 = p.bvh_nodes[2 * i];
         const uint32_t a = __float_as_uint(b0.w);
         float4 b1 = p.bvh_nodes[2 * i + 1];
-        if (!(a & kLeafBitDev)) {
-            b0.w = __uint_as_float(lbase + a * 48u);                 // left child's record
-            b1.w = __uint_as_float(8u * __float_as_uint(b1.w));      // split axis * 8
+        const bool is_leaf = (a & kLeafBitDev) != 0;
+        const uint32_t axis = __float_as_uint(b1.w);  // (leaves: the count)
+        b0.w = __uint_as_float(is_leaf ? ((a & ~kLeafBitDev) << 3) | axis : 0u);
+        b1.w = 0.0f;
+        n4[4 * i] = b0;
+        n4[4 * i + 1] = b1;
+        uint32_t w[8];
+        for (uint32_t o = 0; o < 8; ++o) {
+            const uint32_t miss = addr(g16[8 * i + o]);
+            const uint32_t next = is_leaf ? miss : lbase + (a + ((o >> axis) & 1u)) * 64u;
+            w[o] = next | (miss << 16);
         }
-        n4[3 * i] = b0;
-        n4[3 * i + 1] = b1;
-        uint32_t w[4];
-        for (int k = 0; k < 4; ++k) {
-            const uint32_t l0 = g16[8 * i + 2 * k], l1 = g16[8 * i + 2 * k + 1];
-            w[k] = (l0 == 0xFFFFu ? 0xFFFFu : lbase + l0 * 48u) |
-                   ((l1 == 0xFFFFu ? 0xFFFFu : lbase + l1 * 48u) << 16);
-        }
-        n4[3 * i + 2] = make_float4(__uint_as_float(w[0]), __uint_as_float(w[1]),
-                                    __uint_as_float(w[2]), __uint_as_float(w[3]));
+        n4[4 * i + 2] = make_float4(__uint_as_float(w[0]), __uint_as_float(w[1]), __uint_as_float(w[2]),
+                                    __uint_as_float(w[3]));
+        n4[4 * i + 3] = make_float4(__uint_as_float(w[4]), __uint_as_float(w[5]), __uint_as_float(w[6]),
+                                    __uint_as_float(w[7]));
     }
     for (uint32_t i = threadIdx.x; i < p.nprims; i += blockDim.x) {
         p4[i] = p.bvh_prims[i];
@@ -1097,15 +1119,13 @@ void trace_kernel(TraceParams p) {
                 const SphBound bnd = sph_bound(p, org);
                 F3 nlo, nhi;
                 sphere_slabs(org, inv, sph_inflation(p, bnd, best_t), nlo, nhi);
-                const uint32_t octm = ((oct & 1u) ? 48u : 0u) | ((oct & 2u) ? 48u << 8 : 0u) |
-                                      ((oct & 4u) ? 48u << 16 : 0u);
+                const uint32_t ooff = kLds ? 4u * oct : oct;
 #ifdef RT_WALK_MIX
                 uint32_t wi = 0, wl = 0, wt = 0;
 #endif
                 do {
                     uint32_t leaf;
-                    const bool lf = sphere_node<kLds>(view, inv, oct, octm, best_t, nlo, nhi, node, leaf,
-                                                      node_tests);
+                    const bool lf = sphere_node<kLds>(view, inv, ooff, best_t, nlo, nhi, node, leaf, node_tests);
 #ifdef RT_WALK_MIX
                     if (kCount) {
                         ++wi;
@@ -1115,9 +1135,7 @@ void trace_kernel(TraceParams p) {
                         wt += any2 ? 2u : any1 ? 1u : 0u;
                     }
 #endif
-                    if (lf)
-                        sphere_leaf(p, view, org, dir, inv, leaf, best_t, best_i, bnd, nlo, nhi,
-                                    sph_tests);
+                    if (lf) sphere_leaf(view, org, dir, leaf, best_t, best_i, sph_tests);
                 } while (node != kEnd && (!kStep || --budget != 0));
 #ifdef RT_WALK_MIX
                 if (kCount) {
@@ -2146,13 +2164,12 @@ __device__ __forceinline__ uint32_t serial_trace_b(const TraceParams &p, const B
             const SphBound bnd = sph_bound(p, org);
             F3 nlo, nhi;
             sphere_slabs(org, inv, sph_inflation(p, bnd, best_t), nlo, nhi);
-            const uint32_t octm = ((oct & 1u) ? 48u : 0u) | ((oct & 2u) ? 48u << 8 : 0u) |
-                                  ((oct & 4u) ? 48u << 16 : 0u);
+            const uint32_t ooff = kLds ? 4u * oct : oct;
             uint32_t node = sph_root;
             do {
                 uint32_t leaf;
-                if (sphere_node<kLds>(view, inv, oct, octm, best_t, nlo, nhi, node, leaf, cnt))
-                    sphere_leaf(p, view, org, dir, inv, leaf, best_t, best_i, bnd, nlo, nhi, cnt);
+                if (sphere_node<kLds>(view, inv, ooff, best_t, nlo, nhi, node, leaf, cnt))
+                    sphere_leaf(view, org, dir, leaf, best_t, best_i, cnt);
             } while (node != kEnd);
         } else {
             spheres_brute(p, org, dir, best_t, best_i);

@@ -172,12 +172,12 @@ static int device_for(WorldState &w, int want, DeviceState *&out) {
             d->nnodes = (uint32_t)(bv.nodes.size() / 8);
             d->nbig = (uint32_t)bv.big.size();
             d->nprims = (uint32_t)bv.prim_id.size();
-            // LDS copy of the tree: 48 B per node + 20 B per sphere, u16 links
+            // LDS copy of the tree: 64 B per node + 20 B per sphere, u16 links
             TraceParams lp{};
             lp.nnodes = d->nnodes; lp.nprims = d->nprims; lp.nsph_padded = (uint32_t)p.nsph_padded;
             const size_t lds = trace_lds_bytes(lp);
-            // (the LDS copy addresses 48-B node records with u16 byte offsets)
-            if (d->nnodes <= 65520 / 48 && lds <= env_u64("RT_AMD_LDS_MAX", 64 * 1024)) {
+            // (the LDS copy addresses 64-B node records with u16 byte offsets)
+            if (d->nnodes <= kLdsTreeMaxNodes && lds <= env_u64("RT_AMD_LDS_MAX", 64 * 1024)) {
                 std::vector<uint16_t> m16(bv.miss.size());
                 for (size_t i = 0; i < m16.size(); ++i)
                     m16[i] = bv.miss[i] == kNodeEnd ? (uint16_t)0xFFFF : (uint16_t)bv.miss[i];

@@ -34,7 +34,7 @@ def compile_asm(defs, debug):
 
 def kernel_body(lines, flags):
     """Instruction lines (with their .loc) of trace_kernel<flags>."""
-    tag = "trace_kernelI" + "".join("Lb%sE" % f for f in flags) + "EEvNS_11TraceParamsE:"
+    tag = "trace_kernelI" + "".join(("Li%sE" if k == 3 else "Lb%sE") % f for k, f in enumerate(flags)) + "EEvNS_11TraceParamsE:"
     start = next(i for i, l in enumerate(lines) if l.startswith("_ZN") and tag in l)
     body = []
     loc = None
