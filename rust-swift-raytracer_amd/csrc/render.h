@@ -162,6 +162,12 @@ struct TraceParams {
     FastDiv div_sspp;         // ... and its divider
     uint32_t max_draws;       // 2 + 3 * max(depth, 0): bound of the draw count search
     uint32_t sL, sK;          // kRngSerialPixel: the iteration length and the launch's K
+    // frames of one rank whose global job indices (row * W + col) * spp + s
+    // fit 32 bits (gj32 != 0): the global job of launch job j in local row q is
+    // j + gj_c0 - q * gj_2p (mod 2^32), gj_c0 = (H - 1 - slab_row0) W spp,
+    // gj_2p = 2 W spp -- the refill's job -> (pixel, seed) without the
+    // row-block map and the 64-bit products
+    uint32_t gj32, gj_c0, gj_2p;
 };
 
 // Candidate k of chunk sample jl (frame sample a + jl) means B = serial_lo + k

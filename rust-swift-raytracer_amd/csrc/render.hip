@@ -343,11 +343,23 @@ __device__ __forceinline__ void sphere_slabs(F3 org, F3 inv, float e, F3 &nlo, F
 // to round-4 code) cost ~20 VALU per improvement for boxes ~1 % tighter.
 __device__ __forceinline__ void sphere_leaf(const BvhView &v, F3 org, F3 dir, uint32_t leaf, float &best_t,
                                             int &best_i, uint32_t &sph_tests) {
-    const uint32_t first = leaf >> 3, end = first + (leaf & 7u);
-    for (uint32_t j = first; j < end; ++j) {
+    const uint32_t first = leaf >> 3, n = leaf & 7u;
+#ifndef RT_LEAF_LOOP
+    // leaves hold 1 or 2 spheres (leaf size 2): straight-line tests, the loop
+    // only for larger leaves (RT_AMD_LEAF)
+    sph_tests += n;
+    sphere_candidate(v.prims[first], org, dir, (int)v.ids[first], best_t, best_i);
+    if (n > 1u) {
+        sphere_candidate(v.prims[first + 1], org, dir, (int)v.ids[first + 1], best_t, best_i);
+        for (uint32_t j = first + 2; j < first + n; ++j)
+            sphere_candidate(v.prims[j], org, dir, (int)v.ids[j], best_t, best_i);
+    }
+#else
+    for (uint32_t j = first; j < first + n; ++j) {
         ++sph_tests;
         sphere_candidate(v.prims[j], org, dir, (int)v.ids[j], best_t, best_i);
     }
+#endif
 }
 
 // ------------------------------------------------------------ triangle stage
@@ -1491,7 +1503,18 @@ void trace_kernel(TraceParams p) {
                 // states use the reference's job index below, so the
                 // enumeration order changes no bits.
                 uint32_t s, col, row;
-                job_pixel<kSerial>(pc, job, s, col, row);
+                uint64_t gjob = 0;
+                if (!kSerial && pc.gj32) {
+                    // one rank, 32-bit global jobs (TraceParams::gj32)
+                    const uint32_t lp = fdiv(job, pc.div_spp);
+                    const uint32_t q = fdiv(lp, pc.div_width);
+                    col = lp - q * pc.width;
+                    row = pc.height - 1u - (pc.slab_row0 + q);
+                    gjob = job + pc.gj_c0 - q * pc.gj_2p;
+                } else {
+                    job_pixel<kSerial>(pc, job, s, col, row);
+                    gjob = ((uint64_t)row * pc.width + col) * pc.spp + s;
+                }
                 slot = job + cur_off;
                 bool take = true;
                 if (kSerial) {
@@ -1499,7 +1522,6 @@ void trace_kernel(TraceParams p) {
                     rng = serial_start(pc, job);
                     if (pc.mode == kRngSerialPixel) take = serial_pixel_job(pc, job);
                 } else {
-                    const uint64_t gjob = ((uint64_t)row * pc.width + col) * pc.spp + s;
                     rng = (pc.mode == kRngReplay) ? pc.replay[gjob] : counter_seed(pc.seed, gjob);
                 }
                 // common.rs:335-337: u drawn before v; camera.rs:84-89
@@ -1527,7 +1549,8 @@ void trace_kernel(TraceParams p) {
                         spl0 = 0;
                         spl1 = 0;
                     } else {
-                        const uint2 r = pc.spl[(size_t)(pc.height - 1u - row) * pc.width + col];
+                        // (32-bit index: a frame's pixel count fits)
+                        const uint2 r = pc.spl[(pc.height - 1u - row) * pc.width + col];
                         spl0 = r.x;
                         spl1 = r.y;
                     }

@@ -704,6 +704,9 @@ int render_frame(WorldState &w, const CameraModel &cam, size_t width, size_t hei
         const size_t rows = std::min(rows_per_slab, T - r0);
         const uint64_t njobs = rows * jobs_per_row;
         p.slab_row0 = (uint32_t)r0;
+        p.gj32 = nranks == 1 && (uint64_t)width * height * spp < (1ull << 32) ? 1u : 0u;
+        p.gj_c0 = (uint32_t)(((uint64_t)height - 1 - r0) * width * spp);
+        p.gj_2p = (uint32_t)(2ull * width * spp);
         p.njobs = (uint32_t)njobs;
         p.npix = (uint32_t)(rows * width);
         if (timed) HIP_TRY(hipEventRecord(d->ev[0], s));
