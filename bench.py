@@ -44,6 +44,10 @@ HBM_PEAK_GBS = 8000.0
 ROW_BLOCK = 8  # multi-GPU: row-cyclic blocks of 8 image rows
 
 
+# the frame trace launch's scheduling settings (RtRenderStats.launch_*)
+LAUNCH_KEYS = ("launch_parts", "launch_chunk", "launch_refill_min", "launch_walk_min",
+               "launch_tri_walk_min", "launch_wsteps", "launch_block_threads", "launch_blocks")
+
 NODE_TEST_FLOPS = 26  # slab test: 6 sub, 6 mul, 10 min/max, 4 slack mul/compare
 # triangle node: s = n^.o interval (6 mul, 6 min/max, 4 add), phantom offsets
 # (3 x [4 mul, 6 min/max, 2 mul, 4 add]), slab test (6 sub, 6 mul, 10 min/max, 3 cmp)
@@ -450,6 +454,9 @@ def _report(args, src, world, W, H, spp, depth, st0, rays, elapsed, trace_ms, co
     # machine code (tools/kernel_hash.py) -- the code those counters describe --
     # next to the same hash of the library this run loaded; the whole-.so
     # hashes are reported too
+    # the timed (uncounted) kernel's schedule: profiles record it with their
+    # counters, and the traffic below counts only if it is the same
+    launch = {k[len("launch_"):]: st0[k] for k in LAUNCH_KEYS}
     traffic, tsrc = None, None
     tfile = os.path.join(ROOT, "profiles", "hbm_traffic.json")
     if os.path.exists(tfile):
@@ -466,6 +473,8 @@ def _report(args, src, world, W, H, spp, depth, st0, rays, elapsed, trace_ms, co
                 "benched_trace_kernel_sha256": kloaded,
                 "same_trace_kernel": ent.get("trace_kernel_sha256") is not None
                 and ent.get("trace_kernel_sha256") == kloaded,
+                "profiled_launch": ent.get("launch"),
+                "same_launch_settings": ent.get("launch") == launch,
                 "profiled_lib_sha256": ent.get("lib_sha256"), "benched_lib_sha256": loaded,
                 "same_binary": ent.get("lib_sha256") == loaded}
     ms_per_step = elapsed / args.steps * 1e3
@@ -498,6 +507,7 @@ def _report(args, src, world, W, H, spp, depth, st0, rays, elapsed, trace_ms, co
                      "brute_force_equivalent_tflops": alg_tflops,
                      "algorithmic_hbm_gbs": out_bytes / (trace_ms * 1e-3) / 1e9,
                      "hbm_peak_gbs": HBM_PEAK_GBS},
+        "launch": launch,
         "rays_per_frame": st0["rays"],
         "accel": {1: "brute", 2: "bvh"}.get(st0["accel"], "?"),
         "per_ray": {"sphere_tests": (st0["bvh_sphere_tests"] + st0["big_sphere_tests"]) / st0["rays"],

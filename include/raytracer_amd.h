@@ -114,6 +114,19 @@ typedef struct RtRenderStats {
                                    reference's stream)                          */
   double serial_setup_ms;       /* RT_RNG_SERIAL: HIP-event time of the estimate
                                    pass and its tables (part of serial_ms)      */
+  /* The frame trace launch's scheduling settings (the last launch of the
+   * frame; they decide the schedule, so profiles record them with their
+   * counters): job-queue partitions, jobs per queue pull, refill threshold
+   * (idle lanes), walk gates (sphere / triangle walks), wide-walk fetches per
+   * slice, threads per workgroup and workgroups per launch. */
+  uint32_t launch_parts;
+  uint32_t launch_chunk;
+  uint32_t launch_refill_min;
+  uint32_t launch_walk_min;
+  uint32_t launch_tri_walk_min;
+  uint32_t launch_wsteps;
+  uint32_t launch_block_threads;
+  uint32_t launch_blocks;
 } RtRenderStats;
 
 /* spp 16, depth 8 (lib.rs:51), SERIAL, seed 2547549, one rank, device -1,

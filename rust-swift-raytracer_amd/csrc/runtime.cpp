@@ -59,6 +59,9 @@ DeviceState::~DeviceState() {
         if (b) (void)hipFree(b);
     for (hipEvent_t e : ev)
         if (e) (void)hipEventDestroy(e);
+    for (hipEvent_t e : tev)
+        if (e) (void)hipEventDestroy(e);
+    if (hrec) (void)hipHostFree(hrec);
     for (hipEvent_t e : sev)
         if (e) (void)hipEventDestroy(e);
     if (done) (void)hipEventDestroy(done);
@@ -384,7 +387,7 @@ static int device_sphere_lists(WorldState &w, DeviceState *d, const CameraModel 
 
 int render_frame(WorldState &w, const CameraModel &cam, size_t width, size_t height,
                  const RtRenderOptions &o, uint32_t *d_out, hipStream_t stream,
-                 RtRenderStats *stats, const SerialPass *sp, const uint32_t *d_replay) {
+                 RtRenderStats *stats, const SerialPass *sp, const uint32_t *d_replay, bool defer_stats) {
     if (stats) std::memset(stats, 0, sizeof(*stats));
     const uint32_t nranks = o.nranks ? o.nranks : 1;
     if (o.rank >= nranks) { set_error("rank >= nranks"); return -1; }
@@ -624,7 +627,6 @@ int render_frame(WorldState &w, const CameraModel &cam, size_t width, size_t hei
     const int fam = p.ntri == 0 ? 0 : p.tnodes == 0 ? 1 : (p.tw_nodes != nullptr && ctv != 2) ? 3 : 2;
     const uint64_t waves_per_block = trace_block_threads(use_bvh && p.use_lds, fam, ctv) / 64;
     const uint64_t full_blocks = (uint64_t)bpc * (uint64_t)d->num_cus;
-    double trace_ms = 0.0, resolve_ms = 0.0;
     uint32_t launches = 0, waves = 0;
     // counters only when asked for: one 16-slot record per wave, summed here
     const uint64_t max_waves = full_blocks * waves_per_block;
@@ -700,8 +702,64 @@ int render_frame(WorldState &w, const CameraModel &cam, size_t width, size_t hei
         d->last_jobs = 0;  // the slab holds counts now, not samples
         return 0;
     }
-    for (size_t r0 = 0; r0 < T; r0 += rows_per_slab) {
+    // One frame launch's schedule for kernel kind k (0 lean, 1 counting):
+    // workgroups, waves, jobs per queue pull (chunk) and job-queue partitions
+    struct LaunchPlan { uint64_t blocks, nwaves, chunk, parts, block_threads; };
+    auto plan = [&](int k, uint64_t njobs) -> LaunchPlan {
+        const int kb = !use_bvh ? d->blocks_per_cu[k][sv] : p.use_lds ? d->blocks_per_cu_lds[k][sv]
+                                                                     : d->blocks_per_cu_bvh[k][sv];
+        const uint64_t wpb = trace_block_threads(use_bvh && p.use_lds, fam, k) / 64;
+        const uint64_t jobs_per_block = wpb * 256;
+        uint64_t blocks = std::min<uint64_t>((uint64_t)kb * d->num_cus, (njobs + jobs_per_block - 1) / jobs_per_block);
+        blocks = std::max<uint64_t>(blocks, 1);
+        const uint64_t nwaves = blocks * wpb;
+        uint64_t chunk = env_u64("RT_AMD_CHUNK", 0);
+        if (!chunk) chunk = std::min<uint64_t>(256, std::max<uint64_t>(64, njobs / (nwaves * 16) / 64 * 64));
+        // whole pixels per chunk (partitions are pixel-aligned too), so a
+        // chunk's pixels are complete once its samples are
+        chunk = chunk >= spp ? chunk / spp * spp : spp;
+        if (fused) {
+            // a resolve sums one pixel per lane, so whole-walk kernels take
+            // chunks of >= 8 pixels (<= 4096 jobs unless spp is larger;
+            // A/B, C2: 4 px 7.10 ms, 8 px 6.79, 16 px 6.83, 32 px 7.36,
+            // slab + resolve_kernel 6.94).  Sliced walks keep their chunk
+            // (C5: 16 px +1.5 %, 4 px = slab)
+            uint64_t px = std::max<uint64_t>(1, std::min<uint64_t>(
+                env_u64("RT_AMD_RESOLVE_PIX", p.step ? 1 : 8), 4096 / spp));
+            // small launches (multi-GPU tiles) keep >= 32 chunks per wave
+            // where 4-pixel chunks allow it (C2 tile of 8 ranks: 8 px 1.12 ms,
+            // 4 px 1.04, 2 px 1.22; C3 tile of 8 ranks, 21 chunks of 8 px per
+            // wave: 8 px 9.80 ms, 4 px 9.17, 2 px 9.32; of 4 ranks, 42: 8 and
+            // 4 px 18.0 ms; of 2 ranks: 8 px 35.0, 4 px 35.5)
+            while (px > 4 && njobs / (nwaves * px * spp) < 32) px /= 2;
+            chunk = std::max<uint64_t>(chunk, px * spp);
+        }
+        // job-queue partitions: each keeps >= 16 chunks.  Whole-walk
+        // kernels take 8: a wave whose partition is drained probes the
+        // others one atomic at a time, so at the end of a launch fewer
+        // partitions drain faster (A/B, round 2, C2: 64 -> 5.42 ms, 32 ->
+        // 5.38, 16 -> 5.35, 8 -> 5.36; round 4, 8192 waves of 1024-thread
+        // workgroups, lean frames: 16 -> 4.453 ms, 12 -> 4.335, 10 -> 4.331,
+        // 8 -> 4.346, 4 -> +6 % on the tiles; 8-rank tile 16 -> 0.78, 8 ->
+        // 0.76 ms; C3 62.44 -> 62.37 ms).  Sliced walks keep 64 (C5: 16
+        // costs +1.6 %).
+        uint64_t parts = env_u64("RT_AMD_PARTS", p.step ? 64 : 8);
+        parts = std::max<uint64_t>(1, std::min<uint64_t>({parts, kMaxParts, njobs / (16 * chunk) + 1}));
+        return LaunchPlan{blocks, nwaves, chunk, parts, wpb * 64};
+    };
+    LaunchPlan lean_plan{0, 0, 0, 0, 0};  // the uncounted (timed) kernel's schedule of the last launch
+    uint32_t nslab = 0;  // (counted frames: event triple per launch)
+    for (size_t r0 = 0; r0 < T; r0 += rows_per_slab, ++nslab) {
         const size_t rows = std::min(rows_per_slab, T - r0);
+        hipEvent_t *ev3 = nullptr;
+        if (timed) {
+            while (d->tev.size() < 3 * (size_t)(nslab + 1)) {
+                hipEvent_t e;
+                HIP_TRY(hipEventCreate(&e));
+                d->tev.push_back(e);
+            }
+            ev3 = &d->tev[3 * (size_t)nslab];
+        }
         const uint64_t njobs = rows * jobs_per_row;
         p.slab_row0 = (uint32_t)r0;
         p.gj32 = nranks == 1 && (uint64_t)width * height * spp < (1ull << 32) ? 1u : 0u;
@@ -709,33 +767,10 @@ int render_frame(WorldState &w, const CameraModel &cam, size_t width, size_t hei
         p.gj_2p = (uint32_t)(2ull * width * spp);
         p.njobs = (uint32_t)njobs;
         p.npix = (uint32_t)(rows * width);
-        if (timed) HIP_TRY(hipEventRecord(d->ev[0], s));
+        if (timed) HIP_TRY(hipEventRecord(ev3[0], s));
         if (njobs) {
-            const uint64_t jobs_per_block = waves_per_block * 256;
-            uint64_t blocks = std::min<uint64_t>(full_blocks, (njobs + jobs_per_block - 1) / jobs_per_block);
-            blocks = std::max<uint64_t>(blocks, 1);
-            const uint64_t nwaves = blocks * waves_per_block;
-            uint64_t chunk = env_u64("RT_AMD_CHUNK", 0);
-            if (!chunk) chunk = std::min<uint64_t>(256, std::max<uint64_t>(64, njobs / (nwaves * 16) / 64 * 64));
-            // whole pixels per chunk (partitions are pixel-aligned too), so a
-            // chunk's pixels are complete once its samples are
-            chunk = chunk >= spp ? chunk / spp * spp : spp;
-            if (fused) {
-                // a resolve sums one pixel per lane, so whole-walk kernels take
-                // chunks of >= 8 pixels (<= 4096 jobs unless spp is larger;
-                // A/B, C2: 4 px 7.10 ms, 8 px 6.79, 16 px 6.83, 32 px 7.36,
-                // slab + resolve_kernel 6.94).  Sliced walks keep their chunk
-                // (C5: 16 px +1.5 %, 4 px = slab)
-                uint64_t px = std::max<uint64_t>(1, std::min<uint64_t>(
-                    env_u64("RT_AMD_RESOLVE_PIX", p.step ? 1 : 8), 4096 / spp));
-                // small launches (multi-GPU tiles) keep >= 32 chunks per wave
-                // where 4-pixel chunks allow it (C2 tile of 8 ranks: 8 px 1.12 ms,
-                // 4 px 1.04, 2 px 1.22; C3 tile of 8 ranks, 21 chunks of 8 px per
-                // wave: 8 px 9.80 ms, 4 px 9.17, 2 px 9.32; of 4 ranks, 42: 8 and
-                // 4 px 18.0 ms; of 2 ranks: 8 px 35.0, 4 px 35.5)
-                while (px > 4 && njobs / (nwaves * px * spp) < 32) px /= 2;
-                chunk = std::max<uint64_t>(chunk, px * spp);
-            }
+            const LaunchPlan lp = plan(ctv, njobs);
+            const uint64_t blocks = lp.blocks, nwaves = lp.nwaves, chunk = lp.chunk, parts = lp.parts;
             p.chunk = (uint32_t)chunk;
             p.ring = nullptr;
             p.ring_shift = 0;
@@ -744,69 +779,120 @@ int render_frame(WorldState &w, const CameraModel &cam, size_t width, size_t hei
                 HIP_TRY(grow(d->ring, d->ring_cap, nwaves * 3 * (kTraceRing << p.ring_shift)));
                 p.ring = d->ring;
             }
-            // job-queue partitions: each keeps >= 16 chunks.  Whole-walk
-            // kernels take 8: a wave whose partition is drained probes the
-            // others one atomic at a time, so at the end of a launch fewer
-            // partitions drain faster (A/B, round 2, C2: 64 -> 5.42 ms, 32 ->
-            // 5.38, 16 -> 5.35, 8 -> 5.36; round 4, 8192 waves of 1024-thread
-            // workgroups, lean frames: 16 -> 4.453 ms, 12 -> 4.335, 10 -> 4.331,
-            // 8 -> 4.346, 4 -> +6 % on the tiles; 8-rank tile 16 -> 0.78, 8 ->
-            // 0.76 ms; C3 62.44 -> 62.37 ms).  Sliced walks keep 64 (C5: 16
-            // costs +1.6 %).
-            uint64_t parts = env_u64("RT_AMD_PARTS", p.step ? 64 : 8);
-            parts = std::max<uint64_t>(1, std::min<uint64_t>({parts, kMaxParts, njobs / (16 * chunk) + 1}));
             p.nparts = (uint32_t)parts;
             HIP_TRY(hipMemsetAsync(d->counter, 0, parts * 128, s));
             HIP_TRY(launch_trace(p, (uint32_t)blocks, s));
+            lean_plan = ctv == 0 ? lp : plan(0, njobs);
             d->last_jobs = fused ? 0 : njobs;
             d->last_spp = spp;
             d->last_fused = fused;  // rt_read_samples needs the slab
             ++launches;
             waves = (uint32_t)nwaves;
         }
-        if (timed) HIP_TRY(hipEventRecord(d->ev[1], s));
+        if (timed) HIP_TRY(hipEventRecord(ev3[1], s));
         if (!fused)  // (spp 0: no samples, the resolve still writes every pixel)
             HIP_TRY(launch_resolve_ex(d->samples, d_out, (uint32_t)(rows * width), spp, inv_spp,
                                       (uint32_t)width, (uint32_t)r0, s));
-        if (timed) {
-            HIP_TRY(hipEventRecord(d->ev[2], s));
-            HIP_TRY(hipEventSynchronize(d->ev[2]));
-            float a = 0, b = 0;
-            HIP_TRY(hipEventElapsedTime(&a, d->ev[0], d->ev[1]));
-            HIP_TRY(hipEventElapsedTime(&b, d->ev[1], d->ev[2]));
-            trace_ms += a;
-            resolve_ms += b;
-        }
+        if (timed) HIP_TRY(hipEventRecord(ev3[2], s));
     }
     HIP_TRY(hipEventRecord(d->done, s));
     d->done_stream = s;
     // without stats the frame stays asynchronous on the stream (no host wait)
     if (!timed) return 0;
-    std::vector<unsigned long long> rec(max_waves * kStatSlots);
-    HIP_TRY(hipMemcpyAsync(rec.data(), d->stats, rec.size() * 8, hipMemcpyDeviceToHost, s));
-    HIP_TRY(hipStreamSynchronize(s));
+    // the wave records into pinned host memory (an asynchronous copy, so a
+    // deferred frame does not wait here)
+    const size_t nrec = max_waves * kStatSlots;
+    if (d->hrec_cap < nrec) {
+        if (d->hrec) HIP_TRY(hipHostFree(d->hrec));
+        d->hrec = nullptr;
+        d->hrec_cap = 0;
+        HIP_TRY(hipHostMalloc((void **)&d->hrec, nrec * 8));
+        d->hrec_cap = nrec;
+    }
+    HIP_TRY(hipMemcpyAsync(d->hrec, d->stats, nrec * 8, hipMemcpyDeviceToHost, s));
+    auto &pd = d->pend;
+    pd.active = true;
+    pd.nrec = nrec;
+    pd.nslab = nslab;
+    pd.launches = launches;
+    pd.samples = (uint64_t)T * jobs_per_row;
+    pd.use_bvh = use_bvh;
+    pd.use_tbvh = use_tbvh;
+    pd.stream = s;
+    RtRenderStatsFixed &fx = pd.fixed;
+    fx = RtRenderStatsFixed{};
+    fx.waves = waves;
+    fx.accel = (use_bvh || use_tbvh) ? RT_ACCEL_BVH : RT_ACCEL_BRUTE;
+    fx.tri_bvh = use_tbvh ? 1u : 0u;
+    fx.fused_resolve = fused ? 1u : 0u;
+    fx.primary_lists = primary_lists ? 1u : 0u;
+    fx.camera_tree = p.cam_tris != nullptr ? 1u : 0u;  // camera-origin records (tree or lists)
+    // (the schedule of the frame's uncounted kernel: what a timed frame runs)
+    fx.launch_parts = (uint32_t)lean_plan.parts;
+    fx.launch_chunk = (uint32_t)lean_plan.chunk;
+    fx.launch_refill_min = p.refill_min;
+    fx.launch_walk_min = p.walk_min;
+    fx.launch_tri_walk_min = p.tri_walk_min;
+    fx.launch_wsteps = p.wsteps;
+    fx.launch_block_threads = (uint32_t)lean_plan.block_threads;
+    fx.launch_blocks = (uint32_t)lean_plan.blocks;
+    fx.nsph = d->nsph;
+    fx.ntri = d->ntri;
+    fx.nbig = d->nbig;
+    if (defer_stats) return 0;
+    return collect_frame_stats(d, stats);
+}
+
+int collect_frame_stats(DeviceState *d, RtRenderStats *stats) {
+    auto &pd = d->pend;
+    if (!pd.active) {
+        set_error("no counted frame pending on this device");
+        return -1;
+    }
+    pd.active = false;
+    HIP_TRY(hipSetDevice(d->device));
+    HIP_TRY(hipStreamSynchronize(pd.stream));
+    double trace_ms = 0.0, resolve_ms = 0.0;
+    for (uint32_t k = 0; k < pd.nslab; ++k) {
+        float a = 0, b = 0;
+        HIP_TRY(hipEventElapsedTime(&a, d->tev[3 * k], d->tev[3 * k + 1]));
+        HIP_TRY(hipEventElapsedTime(&b, d->tev[3 * k + 1], d->tev[3 * k + 2]));
+        trace_ms += a;
+        resolve_ms += b;
+    }
+    const unsigned long long *rec = d->hrec;
     if (const char *dump = std::getenv("RT_AMD_WAVE_DUMP")) {  // diagnostic: raw per-wave records
         if (FILE *f = std::fopen(dump, "wb")) {
-            std::fwrite(rec.data(), 8, rec.size(), f);
+            std::fwrite(rec, 8, pd.nrec, f);
             std::fclose(f);
         }
     }
     unsigned long long st[kStatSlots] = {};
-    for (size_t i = 0; i < rec.size(); ++i) st[i % kStatSlots] += rec[i];
+    for (size_t i = 0; i < pd.nrec; ++i) st[i % kStatSlots] += rec[i];
     if (stats) {
-        stats->samples = (uint64_t)T * jobs_per_row;
+        const RtRenderStatsFixed &fx = pd.fixed;
+        const bool use_bvh = pd.use_bvh, use_tbvh = pd.use_tbvh;
+        stats->samples = pd.samples;
         stats->rays = st[0];
-        stats->sphere_tests = st[0] * (uint64_t)d->nsph;
-        stats->tri_tests = st[0] * (uint64_t)d->ntri;  // the reference's brute-force count
+        stats->sphere_tests = st[0] * (uint64_t)fx.nsph;
+        stats->tri_tests = st[0] * (uint64_t)fx.ntri;  // the reference's brute-force count
         stats->tri_in_range = st[1];
         stats->trace_ms = trace_ms;
         stats->resolve_ms = resolve_ms;
-        stats->trace_launches = launches;
-        stats->waves = waves;
-        stats->accel = (use_bvh || use_tbvh) ? RT_ACCEL_BVH : RT_ACCEL_BRUTE;
+        stats->trace_launches = pd.launches;
+        stats->waves = fx.waves;
+        stats->launch_parts = fx.launch_parts;
+        stats->launch_chunk = fx.launch_chunk;
+        stats->launch_refill_min = fx.launch_refill_min;
+        stats->launch_walk_min = fx.launch_walk_min;
+        stats->launch_tri_walk_min = fx.launch_tri_walk_min;
+        stats->launch_wsteps = fx.launch_wsteps;
+        stats->launch_block_threads = fx.launch_block_threads;
+        stats->launch_blocks = fx.launch_blocks;
+        stats->accel = fx.accel;
         stats->bvh_sphere_tests = st[2];
         stats->bvh_node_tests = st[3];
-        stats->big_sphere_tests = use_bvh ? st[0] * (uint64_t)d->nbig : st[0] * (uint64_t)d->nsph;
+        stats->big_sphere_tests = use_bvh ? st[0] * (uint64_t)fx.nbig : st[0] * (uint64_t)fx.nsph;
         for (int k = 0; k < 4; ++k) stats->stamp_cycles[k] = st[4 + k];
 #ifdef RT_STAMPS
         {   // fine segments (tools/stamps.py parses this line)
@@ -828,10 +914,10 @@ int render_frame(WorldState &w, const CameraModel &cam, size_t width, size_t hei
                          "%llu other (%.1f lanes)\n", st[10], st[12] / std::max(1.0, (double)st[10]), st[11],
                          st[13] / std::max(1.0, (double)st[11]), st[10] - st[11],
                          (st[12] - st[13]) / std::max(1.0, (double)(st[10] - st[11])));
-        stats->tri_bvh = use_tbvh ? 1u : 0u;
-        stats->fused_resolve = fused ? 1u : 0u;
-        stats->primary_lists = primary_lists ? 1u : 0u;
-        stats->camera_tree = p.cam_tris != nullptr ? 1u : 0u;  // camera-origin records (tree or lists)
+        stats->tri_bvh = fx.tri_bvh;
+        stats->fused_resolve = fx.fused_resolve;
+        stats->primary_lists = fx.primary_lists;
+        stats->camera_tree = fx.camera_tree;
         stats->bvh_tri_tests = use_tbvh ? st[9] : stats->tri_tests;
     }
     return 0;
@@ -1449,8 +1535,10 @@ int render_frame_multi(WorldState &w, const CameraModel &cam, size_t width, size
             NCCL_TRY(ncclGroupEnd());
         }
     }
-    // every device renders its row blocks (asynchronously unless stats are
-    // wanted: counters need a host wait per device)
+    // every device renders its row blocks, all enqueued before any host wait:
+    // a counted frame leaves its counters pending on its device
+    // (render_frame defer_stats) and they are collected once every device's
+    // tile is in flight, so counted frames keep the timed frames' schedule
     for (uint32_t g = 0; g < n; ++g) {
         RtRenderOptions og = o;
         og.ndevices = 0;
@@ -1465,9 +1553,15 @@ int render_frame_multi(WorldState &w, const CameraModel &cam, size_t width, size
         RtRenderStats sg;
         HIP_TRY(hipSetDevice(devs[g]));
         rc = render_frame(w, cam, width, height, og, ds[g]->tile, ss[g], stats ? &sg : nullptr, nullptr,
-                          serial ? ds[g]->sstates : nullptr);
+                          serial ? ds[g]->sstates : nullptr, /*defer_stats=*/true);
         if (rc) return rc;
-        if (stats) {
+    }
+    for (uint32_t g = 0; g < n && stats; ++g) {
+        RtRenderStats sg;
+        std::memset(&sg, 0, sizeof(sg));
+        rc = collect_frame_stats(ds[g], &sg);
+        if (rc) return rc;
+        {
             stats->samples += sg.samples; stats->rays += sg.rays;
             stats->sphere_tests += sg.sphere_tests; stats->tri_tests += sg.tri_tests;
             stats->tri_in_range += sg.tri_in_range;
@@ -1481,6 +1575,10 @@ int render_frame_multi(WorldState &w, const CameraModel &cam, size_t width, size
             stats->tri_node_tests += sg.tri_node_tests; stats->bvh_tri_tests += sg.bvh_tri_tests;
             stats->tri_bvh = sg.tri_bvh; stats->fused_resolve = sg.fused_resolve;
             stats->primary_lists = sg.primary_lists; stats->camera_tree = sg.camera_tree;
+            stats->launch_parts = sg.launch_parts; stats->launch_chunk = sg.launch_chunk;
+            stats->launch_refill_min = sg.launch_refill_min; stats->launch_walk_min = sg.launch_walk_min;
+            stats->launch_tri_walk_min = sg.launch_tri_walk_min; stats->launch_wsteps = sg.launch_wsteps;
+            stats->launch_block_threads = sg.launch_block_threads; stats->launch_blocks = sg.launch_blocks;
         }
     }
     // RCCL gather of equal-size tiles to the first device (over xGMI); with one

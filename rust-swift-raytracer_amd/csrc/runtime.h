@@ -9,6 +9,7 @@
 #include <mutex>
 #include <memory>
 #include <string>
+#include <vector>
 
 #include "bvh.h"
 #include "render.h"
@@ -18,6 +19,15 @@ struct RtRenderOptions;
 struct RtRenderStats;
 
 namespace rtamd {
+
+// The RtRenderStats fields of a counted frame that the host knows when it
+// enqueues the frame (the rest come from the device's wave records).
+struct RtRenderStatsFixed {
+    uint32_t waves = 0, accel = 0, tri_bvh = 0, fused_resolve = 0, primary_lists = 0, camera_tree = 0;
+    uint32_t launch_parts = 0, launch_chunk = 0, launch_refill_min = 0, launch_walk_min = 0;
+    uint32_t launch_tri_walk_min = 0, launch_wsteps = 0, launch_block_threads = 0, launch_blocks = 0;
+    uint32_t nsph = 0, ntri = 0, nbig = 0;
+};
 
 void set_error(const std::string &msg);
 const std::string &last_error();
@@ -91,6 +101,22 @@ struct DeviceState {
     // [count][step]: workgroups per CU of each kernel instance
     int blocks_per_cu[3][2] = {}, blocks_per_cu_bvh[3][2] = {}, blocks_per_cu_lds[3][2] = {};
     int num_cus = 0;
+    // a counted frame's timing events (3 per launch: start, trace end, resolve
+    // end) and its wave records copied to pinned host memory; with
+    // render_frame(..., defer_stats) the host collects them later
+    // (collect_frame_stats), so several devices' counted frames run at once
+    std::vector<hipEvent_t> tev;
+    unsigned long long *hrec = nullptr; size_t hrec_cap = 0;
+    struct PendingStats {
+        bool active = false;
+        size_t nrec = 0;          // records (waves x kStatSlots) in hrec
+        uint32_t nslab = 0;       // event triples in tev (one per slab)
+        uint32_t launches = 0;    // trace launches
+        uint64_t samples = 0;
+        bool use_bvh = false, use_tbvh = false;
+        RtRenderStatsFixed fixed; // the fields known before the frame ran
+        hipStream_t stream = nullptr;
+    } pend;
     size_t last_jobs = 0;                                       // jobs of the last launch
     size_t last_spp = 0;                                        // and its spp
     bool last_fused = false;                                    // it resolved in-kernel (no slab)
@@ -151,10 +177,15 @@ struct SerialPass {
 // (RGBA8 words, tile row-major).  stream may be null (library stream).
 // sp: launch that SERIAL pass instead (d_out unused).  d_replay: REPLAY from
 // this device-resident start-state table (frame sample order).
+// defer_stats (with stats): the counted frame is only enqueued, and its
+// counters and times are left pending on its device until
+// collect_frame_stats(device state) fills stats.
 int render_frame(WorldState &w, const CameraModel &cam, size_t width, size_t height,
                  const RtRenderOptions &opts, uint32_t *d_out, hipStream_t stream,
                  RtRenderStats *stats, const SerialPass *sp = nullptr,
-                 const uint32_t *d_replay = nullptr);
+                 const uint32_t *d_replay = nullptr, bool defer_stats = false);
+// Waits for device d's pending counted frame and fills stats from it.
+int collect_frame_stats(DeviceState *d, RtRenderStats *stats);
 
 // RT_RNG_SERIAL: the reference's single frame-wide xorshift32 stream
 // (common.rs:321).  Finds every sample's start state on the device (chunked

@@ -71,7 +71,11 @@ class RenderStats(C.Structure):
                 ("serial_retries", C.c_uint32), ("primary_lists", C.c_uint32),
                 ("camera_tree", C.c_uint32), ("serial_iterations", C.c_uint32),
                 ("serial_checked", C.c_uint64), ("serial_chain_breaks", C.c_uint64),
-                ("serial_setup_ms", C.c_double)]
+                ("serial_setup_ms", C.c_double),
+                ("launch_parts", C.c_uint32), ("launch_chunk", C.c_uint32),
+                ("launch_refill_min", C.c_uint32), ("launch_walk_min", C.c_uint32),
+                ("launch_tri_walk_min", C.c_uint32), ("launch_wsteps", C.c_uint32),
+                ("launch_block_threads", C.c_uint32), ("launch_blocks", C.c_uint32)]
 
     def as_dict(self):
         out = {}

@@ -43,6 +43,12 @@ def test_ndevices_one_equals_single_device(scene, w, h, spp):
     out, st1 = world.render(w, h, spp, 8, ndevices=1)
     assert_bits_equal(out, ref, "ndevices=1 frame")
     assert st1["rays"] == st["rays"] and st1["samples"] == st["samples"]
+    # the counted multi-device frame reports the schedule its devices ran (the
+    # uncounted kernel's launch settings), which a single-device frame shares;
+    # its counters are collected after every device's tile was enqueued
+    launch = [k for k in st if k.startswith("launch_")]
+    assert len(launch) == 8 and all(st1[k] == st[k] for k in launch), (st, st1)
+    assert st["launch_blocks"] > 0 and st["launch_parts"] >= 1 and st["launch_chunk"] % spp == 0
     lean, _ = world.render(w, h, spp, 8, ndevices=1, stats=False)
     assert_bits_equal(lean, ref, "ndevices=1 frame without counters")
     with pytest.raises(R.RenderError, match="rank/nranks"):

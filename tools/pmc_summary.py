@@ -59,6 +59,16 @@ def main(src, dst, config="c2"):
             k["hbm_fetch_bytes_x2"] = 2 * k["FETCH_SIZE"] * 1024
             k["hbm_write_bytes"] = k["WRITE_SIZE"] * 1024
             k["hbm_bytes_per_launch"] = k["hbm_fetch_bytes_x2"] + k["hbm_write_bytes"]
+    # the bench line of the kernel-trace pass: the profiled run's schedule
+    # (launch settings) and its timing, kept with the counters
+    logf = os.path.join(src, "trace.log")
+    if os.path.exists(logf):
+        for line in open(logf):
+            if line.startswith("{") and '"metric"' in line:
+                b = json.loads(line)
+                out["launch"] = b.get("launch")
+                out["bench_ms_per_step"] = b.get("ms_per_step")
+                out["bench_avg_launch_ms"] = (b.get("roofline") or {}).get("avg_launch_ms")
     with open(os.path.join(dst, "summary.json"), "w") as fh:
         json.dump(out, fh, indent=1)
     tr = out["kernels"].get("trace_kernel", {})
@@ -68,7 +78,8 @@ def main(src, dst, config="c2"):
         allc[config] = {"trace_bytes_per_launch": tr["hbm_bytes_per_launch"],
                         "from": os.path.relpath(dst, os.path.dirname(path)),
                         "lib_sha256": out.get("lib_sha256"),
-                        "trace_kernel_sha256": out.get("kernel_sha256")}
+                        "trace_kernel_sha256": out.get("kernel_sha256"),
+                        "launch": out.get("launch")}
         with open(path, "w") as fh:
             json.dump(allc, fh, indent=1)
     print(json.dumps(out, indent=1))
