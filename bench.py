@@ -507,7 +507,7 @@ def _report(args, src, world, W, H, spp, depth, st0, rays, elapsed, trace_ms, co
                      "brute_force_equivalent_tflops": alg_tflops,
                      "algorithmic_hbm_gbs": out_bytes / (trace_ms * 1e-3) / 1e9,
                      "hbm_peak_gbs": HBM_PEAK_GBS},
-        "launch": launch,
+        "launch_settings": launch,
         "rays_per_frame": st0["rays"],
         "accel": {1: "brute", 2: "bvh"}.get(st0["accel"], "?"),
         "per_ray": {"sphere_tests": (st0["bvh_sphere_tests"] + st0["big_sphere_tests"]) / st0["rays"],

@@ -219,7 +219,8 @@ size_t serial_scan_scratch(uint32_t npix);
 // SERIAL mode.  ctrl (u32[8]): {resolved, state at sample a, sum of b (low
 // bits), iterations, a = first unresolved sample, candidates per sample of the
 // next iteration (0: the launch's K), iterations that stopped short, 0}.
-// jump: 64 x 32 u32, column c of M^(2^i) (xorshift32 is linear over GF(2)).  Window: win[i] = xorshift32^i(ctrl[1]) for i < n.
+// jump: kSerialJumpWords u32, column c of M^(2^i), then of M^(kSerialWinPerThread
+// j) and M^(4096 j) (xorshift32 is linear over GF(2)).  Window: win[i] = xorshift32^i(ctrl[1]) for i < n.
 // lo (optional): L u32, the iteration's window bases serial_lo(a, jl) with the
 // iteration's K (ctrl[5] when set, else K), for the count pass
 // (TraceParams::slo) and the walks.
@@ -229,6 +230,11 @@ size_t serial_scan_scratch(uint32_t npix);
 // clamped to pix_emax (the pixel table's row stride).
 // counters (optional): ncounters job-queue counters (32 u32 apart) the next
 // trace pass uses, zeroed here instead of by a fill launch.
+// the jump table: M^(2^i) (i < 64), M^(kSerialWinPerThread j) (j < 4096 /
+// kSerialWinPerThread) and M^(4096 j) (j < 256), 32 u32 each
+constexpr uint32_t kSerialWinPerThread = 4;  // window states per thread (serial_window_kernel)
+constexpr uint32_t kSerialJumpT1 = 4096 / kSerialWinPerThread;
+constexpr uint32_t kSerialJumpWords = 32 * (64 + kSerialJumpT1 + 256);
 hipError_t launch_serial_window(uint32_t *ctrl, const uint32_t *jump, uint32_t *win, uint32_t n,
                                 SerialPred M, uint32_t *lo, uint32_t L, uint32_t K, uint32_t depth,
                                 uint32_t nserial, uint32_t pix_spp, uint32_t pix_emax, uint32_t *counters,
@@ -267,6 +273,13 @@ size_t serial_coalesce_search_lds(uint32_t K, uint32_t depth);
 // search, the block walks are skipped).
 uint32_t serial_walk_block(uint32_t L);
 constexpr uint32_t kMaxWalkBlocks = 4096;  // blocks per iteration (the finish kernel's LDS)
+// fin (serial_walk_finish_kernel's result): 4 header words, a column per block
+constexpr uint32_t kWalkFinWords = 4 + kMaxWalkBlocks;
+// pixel table walks from LDS (lds_rows != 0): samples per block at most, and
+// the u8 rows' LDS budget per workgroup
+constexpr uint32_t kMaxWalkR = 256;
+constexpr uint32_t kWalkLdsRowBytes = 48 * 1024;
+constexpr uint32_t kWalkLdsMaxPix = 72;  // pixels one block's samples touch: (R - 1) / spp + 2
 // path, fin (optional, both or neither): scratch of ceil(L / R) R K u32 for the
 // block walks' recorded paths and 4 + kMaxWalkBlocks u32 for the chain's result; with
 // them the full blocks' states are gathered by a parallel kernel, not re-walked.
@@ -277,13 +290,15 @@ constexpr uint32_t kMaxWalkBlocks = 4096;  // blocks per iteration (the finish k
 // pass and the walks use ctrl[5] when it is set.
 // ptab (optional, with path and fin): the pixel table pass's table (ptab[q *
 // ctrl[7] + e], render.h kRngSerialPixel) read by the block walks directly;
-// table is then unused.
+// table is then unused.  lds_rows (with ptab, nonzero): the block walks stage
+// each block's pixel rows in LDS as u8 (depth < 255; that many bytes per
+// workgroup, <= kWalkLdsRowBytes).
 hipError_t launch_serial_walk(uint32_t *ctrl, const float *table, SerialPred M, const double *V,
                               uint32_t npix, uint32_t spp, float z, float sfloor, const uint32_t *win,
                               uint32_t *states, uint32_t *bend, uint32_t *path, uint32_t *fin,
                               const uint32_t *lo, uint32_t *sbend, uint32_t *sB, uint32_t L, uint32_t Lw,
                               uint32_t K, uint32_t R, uint32_t depth, uint32_t nserial, const float *ptab,
-                              hipStream_t stream);
+                              uint32_t lds_rows, hipStream_t stream);
 // (lo: required; sbend, sB: scratch of serial_super_words(L, K, R) and ceil(L / R) K
 // u32 for the superblock chain)
 uint32_t serial_super_words(uint32_t L, uint32_t K, uint32_t R);

@@ -1796,9 +1796,26 @@ __device__ __forceinline__ uint32_t gf2_apply(const uint32_t *cols, uint32_t x) 
     return y;
 }
 
-// Window: thread t writes win[16t, 16t + 16): one jump to 16t (matrices of the
-// set bits), then plain xorshift steps.
-constexpr uint32_t kWinPerThread = 16;
+// the same from a matrix in global memory (tabulated powers), 16-B loads
+__device__ __forceinline__ uint32_t gf2_apply_g(const uint32_t *cols, uint32_t x) {
+    const uint4 *c4 = reinterpret_cast<const uint4 *>(cols);
+    uint32_t y = 0;
+#pragma unroll
+    for (uint32_t q = 0; q < 8u; ++q) {
+        const uint4 m = c4[q];
+        y ^= (x >> (4u * q) & 1u) ? m.x : 0u;
+        y ^= (x >> (4u * q + 1u) & 1u) ? m.y : 0u;
+        y ^= (x >> (4u * q + 2u) & 1u) ? m.z : 0u;
+        y ^= (x >> (4u * q + 3u) & 1u) ? m.w : 0u;
+    }
+    return y;
+}
+
+// Window: thread t writes win[4t, 4t + 4): one jump to 4t (two tabulated
+// matrices), then plain xorshift steps.  (16 states per thread and one
+// matrix apply per set bit of 16t until round 5: a few dozen workgroups of
+// long jumps, 16 us per iteration on world.txt 960x540x16.)
+constexpr uint32_t kWinPerThread = kSerialWinPerThread;
 // It also tabulates the iteration's window bases lo[jl] = serial_lo(a, jl) for
 // jl < L (a = ctrl[4], K = the iteration's candidates), which the count pass
 // and the walks then load instead of evaluating M twice per step.
@@ -1849,7 +1866,12 @@ __global__ __launch_bounds__(256) void serial_window_kernel(uint32_t *__restrict
     const uint32_t i0 = (blockIdx.x * blockDim.x + threadIdx.x) * kWinPerThread;
     if (i0 >= n) return;
     uint32_t x = ctrl[1];
-    for (uint32_t b = 0; (i0 >> b) != 0u; ++b)
+    // the jump to i0: M^(4096 j) M^(4 j') from the tabulated powers (two
+    // applies; were one per set bit of i0, ~7 on average), higher bits by
+    // powers of two
+    x = gf2_apply_g(jump + 32u * (64u + kSerialJumpT1 + ((i0 >> 12) & 255u)), x);
+    x = gf2_apply_g(jump + 32u * (64u + ((i0 & 4095u) / kWinPerThread)), x);
+    for (uint32_t b = 20; (i0 >> b) != 0u; ++b)
         if ((i0 >> b) & 1u) x = gf2_apply(jl_lds + 32u * b, x);
     for (uint32_t q = 0; q < kWinPerThread && i0 + q < n; ++q) {
         win[i0 + q] = x;
@@ -1951,6 +1973,113 @@ __global__ __launch_bounds__(256) void serial_walk_blocks_kernel(
     bend[t] = jl == j1 ? B : kWalkLeft | (jl - j0);
 }
 
+// ---- pixel table walks with the rows in LDS (kRngSerialPixel, depth < 255)
+// One workgroup per block of R samples stages the pixel-table rows of the
+// block's pixels -- positions [plo(q), phi(q)] of each local pixel q, the span
+// its samples' windows cover (serial_pixel_span), as u8 scatter counts -- and
+// then walks from LDS: the per-step reads that were dependent L2 loads (and
+// the path of every candidate, 64 stores per lane) become LDS reads.  A
+// position outside its pixel's traced span reads as "left the window" (the
+// span, not the launch's widest one: positions past a narrower pixel's span
+// were not traced).
+struct WalkRowsLds {
+    uint32_t lo[kMaxWalkR];              // lo[j0 .. j1)
+    uint32_t plo[kWalkLdsMaxPix], span[kWalkLdsMaxPix], off[kWalkLdsMaxPix];
+    uint32_t qa, nq;
+};
+// stages the rows of samples [j0, j1) of the iteration (whole workgroup; E:
+// the pass's positions per pixel, ctrl[7])
+__device__ __forceinline__ void walk_stage_rows(WalkRowsLds &w, uint8_t *rows, uint32_t E, const float *ptab,
+                                                const uint32_t *lo, uint32_t a, uint32_t n, uint32_t j0,
+                                                uint32_t j1, uint32_t K, FastDiv ppix) {
+    const uint32_t spp = ppix.d;
+    const uint32_t p0 = fastdiv_apply(a, ppix);
+    const uint32_t qa = fastdiv_apply(a + j0, ppix) - p0, qb = fastdiv_apply(a + j1 - 1u, ppix) - p0;
+    const uint32_t nq = qb - qa + 1u;
+    for (uint32_t i = threadIdx.x; i < j1 - j0; i += blockDim.x) w.lo[i] = lo[j0 + i];
+    if (threadIdx.x == 0) {
+        w.qa = qa;
+        w.nq = nq;
+        uint32_t off = 0;
+        for (uint32_t i = 0; i < nq; ++i) {
+            const uint32_t q = qa + i;
+            const uint32_t jf = q == 0u ? 0u : (p0 + q) * spp - a;
+            const uint32_t jz = min((p0 + q + 1u) * spp - a, n) - 1u;
+            const uint32_t plo = 2u * jf + 3u * lo[jf];
+            const uint32_t phi = 2u * jz + 3u * (lo[jz] + K - 1u);
+            // the traced positions: plo + e for e < E and plo + e <= phi
+            const uint32_t sp = min(phi >= plo ? phi - plo + 1u : 0u, E);
+            w.plo[i] = plo;
+            w.span[i] = sp;
+            w.off[i] = off;
+            off += sp;
+        }
+    }
+    __syncthreads();
+    for (uint32_t i = 0; i < nq; ++i) {
+        const float *src = ptab + (size_t)(qa + i) * E;
+        uint8_t *dst = rows + w.off[i];
+        for (uint32_t e = threadIdx.x; e < w.span[i]; e += blockDim.x) dst[e] = (uint8_t)src[e];
+    }
+    __syncthreads();
+}
+
+// b of sample jl (local pixel i = q - qa of the rows) at offset B, or -1
+__device__ __forceinline__ int walk_lds_b(const WalkRowsLds &w, const uint8_t *rows, uint32_t i, uint32_t jl,
+                                          uint32_t j0, uint32_t B, uint32_t K) {
+    const uint32_t l = w.lo[jl - j0];
+    const uint32_t pos = 2u * jl + 3u * B;
+    const uint32_t e = pos - w.plo[i];
+    return (B >= l && B - l < K && pos >= w.plo[i] && e < w.span[i]) ? (int)rows[w.off[i] + e] : -1;
+}
+
+// Block walks from LDS rows: bend and path as serial_walk_blocks_kernel (one
+// workgroup of kWalkLdsThreads per block; the pixel's span and row offset stay
+// in registers between pixel changes, so a step is one dependent LDS read).
+constexpr uint32_t kWalkLdsThreads = 1024;
+__global__ __launch_bounds__(kWalkLdsThreads) void serial_walk_blocks_lds_kernel(
+    const uint32_t *__restrict__ ctrl, uint32_t *__restrict__ bend, uint32_t *__restrict__ path,
+    const uint32_t *__restrict__ lo, uint32_t L, uint32_t Kmax, uint32_t R, uint32_t nserial,
+    const float *__restrict__ ptab, FastDiv ppix) {
+    if (ctrl[0] != 0u) return;
+    const uint32_t K = serial_k(ctrl, Kmax);
+    const uint32_t a = ctrl[4];
+    const uint32_t n = min(L, nserial - a);
+    const uint32_t nb = (n + R - 1) / R;
+    const uint32_t blk = blockIdx.x;
+    if (blk >= nb) return;  // (whole workgroups)
+    __shared__ WalkRowsLds w;
+    extern __shared__ uint8_t rows[];
+    const uint32_t j0 = blk * R, j1 = min(j0 + R, n);
+    walk_stage_rows(w, rows, ctrl[7], ptab, lo, a, n, j0, j1, K, ppix);
+    const uint32_t spp = ppix.d, p0 = fastdiv_apply(a, ppix);
+    const size_t stride = (size_t)nb * K;
+    for (uint32_t k0 = threadIdx.x; k0 < K; k0 += blockDim.x) {
+        const size_t t = (size_t)blk * K + k0;
+        uint32_t B = w.lo[0] + k0;
+        uint32_t i = 0;                                     // local pixel of sample jl, - qa
+        uint32_t jnext = (p0 + w.qa + 1u) * spp - a;        // the next pixel's first sample
+        uint32_t plo = w.plo[0], span = w.span[0], off = w.off[0];
+        uint32_t jl = j0;
+        for (; jl < j1; ++jl) {
+            path[(size_t)(jl - j0) * stride + t] = B;
+            if (jl == jnext) {
+                ++i;
+                jnext += spp;
+                plo = w.plo[i];
+                span = w.span[i];
+                off = w.off[i];
+            }
+            const uint32_t l = w.lo[jl - j0];
+            const uint32_t pos = 2u * jl + 3u * B;
+            const uint32_t e = pos - plo;
+            if (!(B >= l && B - l < K && pos >= plo && e < span)) break;
+            B += rows[off + e];
+        }
+        bend[t] = jl == j1 ? B : kWalkLeft | (jl - j0);
+    }
+}
+
 // Superblocks of kSuperBlocks blocks: for every candidate start of a
 // superblock's first block, the chain through its blocks' ends (bend), so that
 // the finish kernel's chain is one dependent load per superblock.  sbend[sb *
@@ -1958,6 +2087,7 @@ __global__ __launch_bounds__(256) void serial_walk_blocks_kernel(
 // where the chain stopped; sB[blk * K + k]: the offset at the start of its
 // block blk (nb * K u32, coalesced over k).
 constexpr uint32_t kSuperBlocks = 16;
+constexpr size_t kSuperLdsBytes = 48 * 1024;  // serial_walk_super_lds_kernel's staged block ends
 __global__ __launch_bounds__(256) void serial_walk_super_kernel(
     const uint32_t *__restrict__ ctrl, const uint32_t *__restrict__ bend, const uint32_t *__restrict__ lo,
     uint32_t *__restrict__ sbend, uint32_t *__restrict__ sB, uint32_t L, uint32_t Kmax, uint32_t R,
@@ -1985,6 +2115,42 @@ __global__ __launch_bounds__(256) void serial_walk_super_kernel(
     sbend[t] = blk == b1 ? B : kWalkLeft | (blk - b0);
 }
 
+// The same with the superblock's block ends staged in LDS (one workgroup per
+// superblock, kSuperBlocks * K u32 <= kSuperLdsBytes): the chain's dependent
+// reads come from LDS instead of L2.
+__global__ __launch_bounds__(1024) void serial_walk_super_lds_kernel(
+    const uint32_t *__restrict__ ctrl, const uint32_t *__restrict__ bend, const uint32_t *__restrict__ lo,
+    uint32_t *__restrict__ sbend, uint32_t *__restrict__ sB, uint32_t L, uint32_t Kmax, uint32_t R,
+    uint32_t nserial) {
+    if (ctrl[0] != 0u) return;
+    const uint32_t K = serial_k(ctrl, Kmax);
+    const uint32_t a = ctrl[4];
+    const uint32_t n = min(L, nserial - a);
+    const uint32_t nb = (n + R - 1) / R;
+    const uint32_t ns = (nb + kSuperBlocks - 1) / kSuperBlocks;
+    const uint32_t sb = blockIdx.x;
+    if (sb >= ns) return;  // (whole workgroups)
+    extern __shared__ uint32_t be[];  // bend of the superblock's blocks, [blk - b0][k]
+    __shared__ uint32_t blo[kSuperBlocks];
+    const uint32_t b0 = sb * kSuperBlocks, b1 = min(nb, b0 + kSuperBlocks);
+    for (uint32_t i = threadIdx.x; i < (b1 - b0) * K; i += blockDim.x) be[i] = bend[(size_t)b0 * K + i];
+    if (threadIdx.x < b1 - b0) blo[threadIdx.x] = lo[(b0 + threadIdx.x) * R];
+    __syncthreads();
+    for (uint32_t k0 = threadIdx.x; k0 < K; k0 += blockDim.x) {
+        uint32_t B = blo[0] + k0;
+        uint32_t blk = b0;
+        for (; blk < b1; ++blk) {
+            sB[(size_t)blk * K + k0] = B;
+            const uint32_t l = blo[blk - b0];
+            if (!(B >= l && B - l < K)) break;
+            const uint32_t e = be[(blk - b0) * K + (B - l)];
+            if (e & kWalkLeft) break;
+            B = e;
+        }
+        sbend[(size_t)sb * K + k0] = blk == b1 ? B : kWalkLeft | (blk - b0);
+    }
+}
+
 __global__ __launch_bounds__(256) void serial_walk_finish_kernel(
     uint32_t *__restrict__ ctrl, const float *__restrict__ table, SerialPred M,
     const double *__restrict__ V, uint32_t npix, uint32_t spp, const uint32_t *__restrict__ win,
@@ -1998,7 +2164,7 @@ __global__ __launch_bounds__(256) void serial_walk_finish_kernel(
     __shared__ uint32_t scol[kMaxWalkBlocks / kSuperBlocks + 1];  // the chain's column in each superblock
     __shared__ uint32_t cB, cblk, cleft;
     if (ctrl[0] != 0u) {
-        if (fin && threadIdx.x == 0) fin[1] = 0u;  // (serial_states_kernel: nothing)
+        if (fin && threadIdx.x == 0) fin[1] = fin[3] = 0u;  // (the states kernels: nothing)
         return;
     }
     const uint32_t K = serial_k(ctrl, Kmax);
@@ -2725,7 +2891,7 @@ hipError_t launch_serial_walk(uint32_t *ctrl, const float *table, SerialPred M, 
                               uint32_t *states, uint32_t *bend, uint32_t *path, uint32_t *fin,
                               const uint32_t *lo, uint32_t *sbend, uint32_t *sB, uint32_t L, uint32_t Lw,
                               uint32_t K, uint32_t R, uint32_t depth, uint32_t nserial, const float *ptab,
-                              hipStream_t stream) {
+                              uint32_t lds_rows, hipStream_t stream) {
     if (!L || !R) return hipSuccess;
     const uint32_t nb = (L + R - 1) / R;
     if (nb > kMaxWalkBlocks) return hipErrorInvalidValue;
@@ -2735,12 +2901,23 @@ hipError_t launch_serial_walk(uint32_t *ctrl, const float *table, SerialPred M, 
     // (the coalescing search and the pixel table need the recorded paths: the
     // finish kernel's lane-serial fallback reads a count table)
     if ((table == nullptr || ptab != nullptr) && !path) return hipErrorInvalidValue;
-    if (table != nullptr || ptab != nullptr)
+    const FastDiv ppix = make_fastdiv(spp ? spp : 1u);
+    // the pixel table's walks from LDS rows (lds_rows bytes per workgroup)
+    if (ptab != nullptr && lds_rows != 0) {
+        if (R > kMaxWalkR) return hipErrorInvalidValue;
+        hipLaunchKernelGGL(serial_walk_blocks_lds_kernel, dim3(nb), dim3(kWalkLdsThreads), lds_rows, stream, ctrl,
+                           bend, path, lo, L, K, R, nserial, ptab, ppix);
+    } else if (table != nullptr || ptab != nullptr) {
         hipLaunchKernelGGL(serial_walk_blocks_kernel, dim3((uint32_t)((nt + 255) / 256)), dim3(256), 0, stream,
-                           ctrl, table, M, bend, path, lo, L, K, R, depth, nserial, ptab,
-                           make_fastdiv(spp ? spp : 1u));
-    hipLaunchKernelGGL(serial_walk_super_kernel, dim3((uint32_t)((nst + 255) / 256)), dim3(256), 0, stream,
-                       ctrl, bend, lo, sbend, sB, L, K, R, nserial);
+                           ctrl, table, M, bend, path, lo, L, K, R, depth, nserial, ptab, ppix);
+    }
+    const uint32_t ns = (nb + kSuperBlocks - 1) / kSuperBlocks;
+    if ((size_t)kSuperBlocks * K * 4 <= kSuperLdsBytes)
+        hipLaunchKernelGGL(serial_walk_super_lds_kernel, dim3(ns), dim3(1024), (size_t)kSuperBlocks * K * 4, stream,
+                           ctrl, bend, lo, sbend, sB, L, K, R, nserial);
+    else
+        hipLaunchKernelGGL(serial_walk_super_kernel, dim3((uint32_t)((nst + 255) / 256)), dim3(256), 0, stream,
+                           ctrl, bend, lo, sbend, sB, L, K, R, nserial);
     hipLaunchKernelGGL(serial_walk_finish_kernel, dim3(1), dim3(256), 0, stream, ctrl, table, M, V, npix,
                        spp ? spp : 1u, win, bend, path, states, path ? fin : nullptr, lo, sbend, sB, L, Lw, K,
                        R, depth, nserial, z, sfloor);

@@ -951,8 +951,12 @@ uint32_t xorshift32(uint32_t x) {
 }
 
 // columns of M^(2^i), i < 64, M the xorshift32 step as a GF(2) matrix
+// xorshift32 jump matrices (GF(2), 32 columns each; render.h
+// kSerialJumpWords): M^(2^i) for i < 64, then M^(w j) for j < 4096 / w (w =
+// kSerialWinPerThread) and M^(4096 j) for j < 256 (serial_window_kernel: two
+// applies reach any multiple of w below 2^20)
 std::vector<uint32_t> xorshift_jump_table() {
-    std::vector<uint32_t> t(64 * 32);
+    std::vector<uint32_t> t(kSerialJumpWords);
     for (uint32_t c = 0; c < 32; ++c) t[c] = xorshift32(1u << c);
     auto apply = [&](const uint32_t *cols, uint32_t x) {
         uint32_t y = 0;
@@ -962,6 +966,17 @@ std::vector<uint32_t> xorshift_jump_table() {
     };
     for (int i = 1; i < 64; ++i)
         for (uint32_t c = 0; c < 32; ++c) t[32 * i + c] = apply(&t[32 * (i - 1)], t[32 * (i - 1) + c]);
+    static_assert((kSerialWinPerThread & (kSerialWinPerThread - 1)) == 0, "a power of two");
+    int wlog = 0;
+    while ((1u << wlog) < kSerialWinPerThread) ++wlog;
+    for (int lvl = 0; lvl < 2; ++lvl) {
+        uint32_t *T = &t[(size_t)32 * (64 + (lvl ? kSerialJumpT1 : 0))];
+        const uint32_t *step = &t[32 * (lvl == 0 ? wlog : 12)];  // M^w, M^4096
+        const uint32_t cnt = lvl == 0 ? kSerialJumpT1 : 256u;
+        for (uint32_t c = 0; c < 32; ++c) T[c] = 1u << c;  // M^0
+        for (uint32_t j = 1; j < cnt; ++j)
+            for (uint32_t c = 0; c < 32; ++c) T[32 * j + c] = apply(step, T[32 * (j - 1) + c]);
+    }
     return t;
 }
 }  // namespace
@@ -1171,6 +1186,15 @@ static int serial_find_states(WorldState &w, const CameraModel &cam, size_t widt
             : pixtab ? std::min<uint64_t>(L, std::max<uint64_t>({env_u64("RT_AMD_SERIAL_WALKR", 64), 1,
                                                                  (L + kMaxWalkBlocks - 1) / kMaxWalkBlocks}))
                      : serial_walk_block((uint32_t)L);
+        // the pixel table's walks read each block's rows from LDS (as u8 counts:
+        // depth < 255) when a block's pixels x the row stride fit the budget
+        // (RT_AMD_SERIAL_WALK_LDS=0: the walks read the table in global memory)
+        uint32_t walk_lds = 0;
+        if (pixtab && !pgather && depth < 255 && R_walk <= kMaxWalkR &&
+            env_u64("RT_AMD_SERIAL_WALK_LDS", 1) != 0) {
+            const uint64_t maxpix = (R_walk - 1) / spp + 2;
+            if (maxpix <= kWalkLdsMaxPix && maxpix * emax <= kWalkLdsRowBytes) walk_lds = (uint32_t)(maxpix * emax);
+        }
         uint32_t K0 = 0;  // the first iteration's candidates (later ones: the walks)
         if (adapt) {
             const double w0 = 2.0 * z * (std::sqrt(std::max(sm[2], 0.0)) + serial_floor(spp * R) * std::sqrt((double)n0));
@@ -1186,7 +1210,7 @@ static int serial_find_states(WorldState &w, const CameraModel &cam, size_t widt
         const bool gather = coalesce || pixtab || env_u64("RT_AMD_SERIAL_GATHER", 1) != 0;
         if (gather) {
             HIP_TRY(grow(d->spath, d->spath_cap, (L + R_walk - 1) / R_walk * R_walk * K));
-            if (!d->sfin) HIP_TRY(hipMalloc((void **)&d->sfin, (4 + kMaxWalkBlocks) * 4));
+            if (!d->sfin) HIP_TRY(hipMalloc((void **)&d->sfin, kWalkFinWords * 4));
         }
         if (!d->sjump) {
             const std::vector<uint32_t> jt = xorshift_jump_table();
@@ -1251,7 +1275,7 @@ static int serial_find_states(WorldState &w, const CameraModel &cam, size_t widt
                                            gather ? d->spath : nullptr, gather ? d->sfin : nullptr, d->slo,
                                            d->ssbend, d->ssb, (uint32_t)L, (uint32_t)Lw, (uint32_t)K,
                                            (uint32_t)R_walk, depth, (uint32_t)N,
-                                           (pixtab && !pgather) ? d->sptab : nullptr, s));
+                                           (pixtab && !pgather) ? d->sptab : nullptr, walk_lds, s));
             }
             const auto t1 = std::chrono::steady_clock::now();
             HIP_TRY(hipMemcpyAsync(ctrl, d->sctrl, 32, hipMemcpyDeviceToHost, s));

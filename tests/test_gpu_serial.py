@@ -108,6 +108,11 @@ def test_serial_narrow_windows_and_short_iterations(monkeypatch):
         (dict(RT_AMD_SERIAL_CHUNK="9"), "world.txt", (13, 7, 16, 8)),
         (dict(RT_AMD_SERIAL_CHUNK="50", RT_AMD_SERIAL_K="8"), "world.txt", (7, 5, 33, 4)),
         (dict(RT_AMD_SERIAL_PCHUNK="1000"), "world.txt", (33, 17, 5, 8)),
+        # LDS-staged rows: blocks of 256 samples over many pixels, a block of one
+        # pixel's samples, 1-sample blocks
+        (dict(RT_AMD_SERIAL_WALKR="256", RT_AMD_SERIAL_CHUNK="3000"), "world.txt", (33, 17, 4, 8)),
+        (dict(RT_AMD_SERIAL_WALKR="16"), "c_raytracer_world.txt", (40, 30, 16, 8)),
+        (dict(RT_AMD_SERIAL_WALKR="1", RT_AMD_SERIAL_CHUNK="200"), "world.txt", (13, 7, 4, 8)),
         # pixel table through a gathered count table (the first build's walks)
         (dict(RT_AMD_SERIAL_PGATHER="1", RT_AMD_SERIAL_K="40"), "c_raytracer_world.txt", (40, 30, 16, 8)),
     ]:
@@ -124,6 +129,9 @@ SEARCHES = {
     # runtime.cpp serial_find_states: the pixel table (default from 4 spp), the
     # count pass + block walks, the coalescing block search
     "pixtab": dict(RT_AMD_SERIAL_PIXTAB="1"),
+    # the pixel table's block walks and state gather reading the table in
+    # global memory instead of LDS-staged u8 rows
+    "pixtab_global": dict(RT_AMD_SERIAL_PIXTAB="1", RT_AMD_SERIAL_WALK_LDS="0"),
     "count": dict(RT_AMD_SERIAL_PIXTAB="0", RT_AMD_SERIAL_COALESCE="0"),
     "coalesce": dict(RT_AMD_SERIAL_PIXTAB="0", RT_AMD_SERIAL_COALESCE="1"),
 }

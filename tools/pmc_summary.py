@@ -66,7 +66,7 @@ def main(src, dst, config="c2"):
         for line in open(logf):
             if line.startswith("{") and '"metric"' in line:
                 b = json.loads(line)
-                out["launch"] = b.get("launch")
+                out["launch"] = b.get("launch_settings")
                 out["bench_ms_per_step"] = b.get("ms_per_step")
                 out["bench_avg_launch_ms"] = (b.get("roofline") or {}).get("avg_launch_ms")
     with open(os.path.join(dst, "summary.json"), "w") as fh:

@@ -214,10 +214,17 @@ static float trace_wide(const TriangleBVH &t, const Wide &W, V o, V d, WideCount
     const float ov[3] = {o.x, o.y, o.z};
     const float dv[3] = {o.x - t.oc[0], o.y - t.oc[1], o.z - t.oc[2]};
     auto dec = [](uint32_t q, float s, float b) { return std::fmaf((float)q, s, b); };
+    // SIM_WIDE_SHARED_N=1: every child of a wide node is widened with the
+    // union of the children's normal boxes (one widening per fetch)
+    static const bool shared_n = std::getenv("SIM_WIDE_SHARED_N") != nullptr;
+    uint32_t shared_m[6] = {0, 0, 0, 0, 0, 0};
+    bool use_shared = false;
     auto box = [&](uint32_t node, float &tn, float &tf) {
         const uint32_t *w = &t.qnodes[(size_t)node * 8];
         const uint32_t u[6] = {w[0] & 0xFFFF, w[0] >> 16, w[1] & 0xFFFF, w[1] >> 16, w[2] & 0xFFFF, w[2] >> 16};
-        const uint32_t m[6] = {w[3] & 0xFFFF, w[3] >> 16, w[4] & 0xFFFF, w[4] >> 16, w[5] & 0xFFFF, w[5] >> 16};
+        uint32_t m[6] = {w[3] & 0xFFFF, w[3] >> 16, w[4] & 0xFFFF, w[4] >> 16, w[5] & 0xFFFF, w[5] >> 16};
+        if (use_shared)
+            for (int k = 0; k < 6; ++k) m[k] = shared_m[k];
         float sl = 0, sh = 0, n0[3], n1[3];
         for (int k = 0; k < 3; ++k) {
             n0[k] = dec(m[k], t.nstep, t.nbase);
@@ -226,10 +233,24 @@ static float trace_wide(const TriangleBVH &t, const Wide &W, V o, V d, WideCount
             sl += std::fmin(a, b); sh += std::fmax(a, b);
         }
         tn = -INFINITY; tf = INFINITY;
+        // SIM_WIDE_SYM=1: symmetric widening 2 S max|m_k|, S = sum_k max|m d_k| >= |s|
+        static const bool sym = std::getenv("SIM_WIDE_SYM") != nullptr;
+        float S = 0;
+        for (int k = 0; k < 3; ++k) S += std::fmax(std::fabs(n0[k] * dv[k]), std::fabs(n1[k] * dv[k]));
         for (int k = 0; k < 3; ++k) {
             float a = sl * n0[k], b = sl * n1[k], cc = sh * n0[k], dd = sh * n1[k];
-            float lo = dec(u[k], t.qbox.step[k], t.qbox.base[k]) + 2 * std::fmin(std::fmin(a, b), std::fmin(cc, dd)) - rho;
-            float hi = dec(u[3 + k], t.qbox.step[k], t.qbox.base[k]) + 2 * std::fmax(std::fmax(a, b), std::fmax(cc, dd)) + rho;
+            float wl = std::fmin(std::fmin(a, b), std::fmin(cc, dd)), wh = std::fmax(std::fmax(a, b), std::fmax(cc, dd));
+            if (sym) { wh = S * std::fmax(std::fabs(n0[k]), std::fabs(n1[k])); wl = -wh; }
+            // SIM_WIDE_MR=1: midpoint-radius enclosure of [sl, sh] x [n0, n1]
+            static const bool mr = std::getenv("SIM_WIDE_MR") != nullptr;
+            if (mr) {
+                const float sc = 0.5f * (sl + sh), sr = 0.5f * (sh - sl);
+                const float mc = 0.5f * (n0[k] + n1[k]), mrr = 0.5f * (n1[k] - n0[k]);
+                const float pm = sc * mc, rad = std::fabs(sc) * mrr + sr * (std::fabs(mc) + mrr);
+                wl = pm - rad; wh = pm + rad;
+            }
+            float lo = dec(u[k], t.qbox.step[k], t.qbox.base[k]) + 2 * wl - rho;
+            float hi = dec(u[3 + k], t.qbox.step[k], t.qbox.base[k]) + 2 * wh + rho;
             float t0 = (lo - ov[k]) * iv[k], t1 = (hi - ov[k]) * iv[k];
             tn = std::fmax(tn, std::fmin(t0, t1));
             tf = std::fmin(tf, std::fmax(t0, t1));
@@ -271,6 +292,19 @@ static float trace_wide(const TriangleBVH &t, const Wide &W, V o, V d, WideCount
         if (etn > best) continue;
         c.fetches += 1;
         std::vector<std::pair<float, uint32_t>> hits;
+        if (shared_n) {
+            // the union of the children's normal boxes (u16 grid words 3..5)
+            for (int k = 0; k < 3; ++k) { shared_m[k] = 0xFFFF; shared_m[3 + k] = 0; }
+            for (uint32_t ch : W.kids[node]) {
+                const uint32_t *w = &t.qnodes[(size_t)ch * 8];
+                const uint32_t m[6] = {w[3] & 0xFFFF, w[3] >> 16, w[4] & 0xFFFF, w[4] >> 16, w[5] & 0xFFFF, w[5] >> 16};
+                for (int k = 0; k < 3; ++k) {
+                    shared_m[k] = std::min(shared_m[k], m[k]);
+                    shared_m[3 + k] = std::max(shared_m[3 + k], m[3 + k]);
+                }
+            }
+            use_shared = true;
+        }
         for (uint32_t ch : W.kids[node]) {
             float tn, tf;
             c.boxes += 1;
@@ -278,6 +312,7 @@ static float trace_wide(const TriangleBVH &t, const Wide &W, V o, V d, WideCount
             if (tn > tf || tf < 0.001f || tn > best) continue;
             hits.push_back({tn, ch});
         }
+        use_shared = false;
         // SIM_WIDE_ORDER=0: slot order (nearest-first otherwise)
         static const bool sorted = !std::getenv("SIM_WIDE_ORDER") || std::atoi(std::getenv("SIM_WIDE_ORDER")) != 0;
         if (sorted) std::sort(hits.begin(), hits.end());
