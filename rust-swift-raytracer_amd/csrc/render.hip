@@ -714,6 +714,13 @@ __device__ __forceinline__ void resolve_store(const TraceParams &p, uint32_t lp,
 // adds per pixel).  Other chunks, and the triangle kernels (kPlaneLanes
 // false: at their 64-VGPR cap the float4 rounds spill, C5 +7 %), sum one
 // pixel per lane.
+// which kernel families fold with plane lanes (RT_PLANE_LANES_WIDE: the wide
+// triangle walk too, A/B)
+#ifdef RT_PLANE_LANES_WIDE
+#define RT_PLANE_LANES(mesh) ((mesh) < 2 || (mesh) == 3)
+#else
+#define RT_PLANE_LANES(mesh) ((mesh) < 2)
+#endif
 template <bool kPlaneLanes>
 __device__ __forceinline__ void resolve_chunk(const TraceParams &p, const float *ring, uint32_t plane,
                                               uint32_t off, uint32_t base, uint32_t len,
@@ -1436,7 +1443,7 @@ void trace_kernel(TraceParams p) {
                     if (n != 0 && rleft[k] == 0) {
                         const TraceParams &pc = kargs();
                         if (!(pc.ablate & 2u))
-                            resolve_chunk<kMesh < 2>(pc, sbase, pstride, k << pc.ring_shift, rbase[k],
+                            resolve_chunk<RT_PLANE_LANES(kMesh)>(pc, sbase, pstride, k << pc.ring_shift, rbase[k],
                                                   rlen[k], lane);
                         rfree |= 1u << k;
                     }
