@@ -714,13 +714,10 @@ __device__ __forceinline__ void resolve_store(const TraceParams &p, uint32_t lp,
 // adds per pixel).  Other chunks, and the triangle kernels (kPlaneLanes
 // false: at their 64-VGPR cap the float4 rounds spill, C5 +7 %), sum one
 // pixel per lane.
-// which kernel families fold with plane lanes (RT_PLANE_LANES_WIDE: the wide
-// triangle walk too, A/B)
-#ifdef RT_PLANE_LANES_WIDE
+// which kernel families fold with plane lanes: the sphere kernels and the
+// wide triangle walk (A/B on C5, 1-pixel chunks: 149.8 -> 148.1 ms, 2 VGPRs
+// spilled); the binary triangle walk keeps one lane per pixel
 #define RT_PLANE_LANES(mesh) ((mesh) < 2 || (mesh) == 3)
-#else
-#define RT_PLANE_LANES(mesh) ((mesh) < 2)
-#endif
 template <bool kPlaneLanes>
 __device__ __forceinline__ void resolve_chunk(const TraceParams &p, const float *ring, uint32_t plane,
                                               uint32_t off, uint32_t base, uint32_t len,
