@@ -93,6 +93,9 @@ __device__ __forceinline__ F3 draw_unit(uint32_t &s) {
 }
 
 __device__ __forceinline__ uint32_t counter_seed(uint32_t seed, uint64_t job) {
+#ifdef RT_ABLATE_SEED  // timing-only diagnostic: wrong seeds
+    return ((uint32_t)job * 0x9E3779B9u + seed) | 1u;
+#endif
     uint64_t z = job + (uint64_t)seed * 0x9E3779B97F4A7C15ull + 0x9E3779B97F4A7C15ull;
     z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
     z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;

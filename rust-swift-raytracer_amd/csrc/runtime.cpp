@@ -1073,9 +1073,14 @@ static int serial_find_states(WorldState &w, const CameraModel &cam, size_t widt
             coalesce = !pixtab && env_u64("RT_AMD_SERIAL_COALESCE", trees ? 0 : 1) != 0 && depth < 1024;
             uint64_t Ldef = coalesce ? 131072 : 16384;
             if (pixtab) {
-                Ldef = 32768;
-                for (uint64_t q = 64; q <= spp; q *= 4) Ldef *= 2;        // 64 spp: 64 k, 256 spp: 128 k
-                for (uint64_t q = spp; q < 16 && Ldef > 8192; q *= 4) Ldef /= 2;  // 4 spp: 16 k
+                // (round 5, after the iterations' fixed cost fell from ~90 to ~54
+                // us: 48 k at 16 spp, profiles/round5_serial/iteration_length_*.log:
+                // world.txt 960x540x16 32 k / 48 k / 64 k / 96 k -> 92.5 / 91.3 /
+                // 94.3 / 102.5 ms, 1920x1080x16 400 / 368 / 385 / 425 ms; RTOW
+                // 1920x1080x64 64 k / 96 k / 128 k -> 732 / 683 / 689 ms)
+                Ldef = 49152;
+                for (uint64_t q = 64; q <= spp; q *= 4) Ldef *= 2;        // 64 spp: 96 k, 256 spp: 192 k
+                for (uint64_t q = spp; q < 16 && Ldef > 8192; q *= 4) Ldef /= 2;  // 4 spp: 24 k
             }
             L = std::max<uint64_t>(1, std::min<uint64_t>(env_u64("RT_AMD_SERIAL_CHUNK", Ldef), N));
             // windows are sized for the deviation over Lw samples (default L; a

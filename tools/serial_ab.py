@@ -70,17 +70,18 @@ def main():
                         os.environ.pop(k, None)
                     else:
                         os.environ[k] = v
+                case = f"{name}:{w}x{h}x{spp}/{depth}"
                 if rnd == 0:
-                    ref.setdefault(name, img)
-                    res[(label, name)] = {"same": bool((img == ref[name]).all()), "wall": [], "search": [],
+                    ref.setdefault(case, img)
+                    res[(label, case)] = {"same": bool((img == ref[case]).all()), "wall": [], "search": [],
                                           "it": st["serial_iterations"], "short": st["serial_retries"]}
                     continue
-                r = res[(label, name)]
+                r = res[(label, case)]
                 r["wall"].append(wall)
                 r["search"].append(st["serial_ms"])
-                r["same"] = r["same"] and bool((img == ref[name]).all())
-    for (label, name), r in res.items():
-        print(json.dumps({"variant": label, "case": name, "wall_ms_median": statistics.median(r["wall"]),
+                r["same"] = r["same"] and bool((img == ref[case]).all())
+    for (label, case), r in res.items():
+        print(json.dumps({"variant": label, "case": case, "wall_ms_median": statistics.median(r["wall"]),
                           "search_ms_median": statistics.median(r["search"]), "iterations": r["it"],
                           "stopped_short": r["short"], "frame_equal_to_first_variant": r["same"]}), flush=True)
 
