@@ -1312,9 +1312,27 @@ void trace_kernel(TraceParams p) {
             if (phase == kShade) {
                 const TraceParams &p = kargs();  // (see kargs)
                 phase = kSetup;
-                if (tri_i < 0 && best_i < 0) {
+                // One NVec3::new for both kinds of lane that need one here: a
+                // missed ray re-normalises its direction (common.rs:277), a
+                // sphere hit normalises (pos - c) / r (common.rs:95), so the
+                // wave runs one copy of the sqrt / divide sequence, not two
+                const bool sky = tri_i < 0 && best_i < 0;
+                const bool sph = tri_i < 0 && best_i >= 0;
+                F3 un = dir, spos = dir;
+                float4 SS = make_float4(0.0f, 0.0f, 0.0f, 0.0f), SM = SS;
+                uint32_t skind = 0;
+                if (sph) {
+                    // one round trip: centre/radius, colour/param and kind together
+                    SS = view.shade[2 * best_i];
+                    SM = view.shade[2 * best_i + 1];
+                    skind = view.kinds[best_i];
+                    spos = org + scale(dir, best_t);
+                    un = divide_by(spos - f3(SS.x, SS.y, SS.z), SS.w);
+                }
+                if (sky || sph) un = unit(un);
+                if (sky) {
                     // background (common.rs:276-281): re-normalise, lerp to sky blue
-                    const float t = 0.5f * (unit(dir).y + 1.0f);
+                    const float t = 0.5f * (un.y + 1.0f);
                     const float w = 1.0f - t;
                     out_r = thr_r * (1.0f * w + 0.5f * t);
                     out_g = thr_g * (1.0f * w + 0.7f * t);
@@ -1333,13 +1351,10 @@ void trace_kernel(TraceParams p) {
                         kind = __float_as_uint(m[0]);
                         cr = m[1]; cg = m[2]; cb = m[3]; param = m[4];
                     } else {
-                        // one round trip: centre/radius, colour/param and kind together
-                        const float4 S = view.shade[2 * best_i];
-                        const float4 M = view.shade[2 * best_i + 1];
-                        kind = view.kinds[best_i];
-                        pos = org + scale(dir, best_t);
-                        nrm = unit(divide_by(pos - f3(S.x, S.y, S.z), S.w));  // common.rs:95
-                        cr = M.x; cg = M.y; cb = M.z; param = M.w;
+                        kind = skind;
+                        pos = spos;
+                        nrm = un;  // common.rs:95, normalised above
+                        cr = SM.x; cg = SM.y; cb = SM.z; param = SM.w;
                     }
                     // Each scatter builds an un-normalised direction `v`; the draws
                     // of diffuse and metal (random_unit_sphere, common.rs:32-38) and
