@@ -726,12 +726,17 @@ int render_frame(WorldState &w, const CameraModel &cam, size_t width, size_t hei
             // (C5: 16 px +1.5 %, 4 px = slab)
             uint64_t px = std::max<uint64_t>(1, std::min<uint64_t>(
                 env_u64("RT_AMD_RESOLVE_PIX", p.step ? 1 : 8), 4096 / spp));
-            // small launches (multi-GPU tiles) keep >= 32 chunks per wave
+            // small launches (multi-GPU tiles) keep >= 16 chunks per wave
             // where 4-pixel chunks allow it (C2 tile of 8 ranks: 8 px 1.12 ms,
             // 4 px 1.04, 2 px 1.22; C3 tile of 8 ranks, 21 chunks of 8 px per
             // wave: 8 px 9.80 ms, 4 px 9.17, 2 px 9.32; of 4 ranks, 42: 8 and
-            // 4 px 18.0 ms; of 2 ranks: 8 px 35.0, 4 px 35.5)
-            while (px > 4 && njobs / (nwaves * px * spp) < 32) px /= 2;
+            // 4 px 18.0 ms; of 2 ranks: 8 px 35.0, 4 px 35.5).  Round 5: 32
+            // until then, which put the full C2 frame (31.6 chunks of 8 px per
+            // wave at 8,192 waves) on 4-pixel chunks: lean frame 3.900 ms
+            // against 3.745 ms with 8, 3.811 with 12 and 3.912 with 16 pixels
+            // (profiles/round5_walk/ab_c2_chunk.jsonl); the 8-rank tile keeps
+            // 4 px (0.678 ms, 8 px 0.849 ms)
+            while (px > 4 && njobs / (nwaves * px * spp) < 16) px /= 2;
             chunk = std::max<uint64_t>(chunk, px * spp);
         }
         // job-queue partitions: each keeps >= 16 chunks.  Whole-walk
