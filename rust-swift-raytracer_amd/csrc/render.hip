@@ -333,6 +333,26 @@ __device__ __forceinline__ bool sphere_node(const BvhView &v, F3 inv, uint32_t o
     return !skip && is_leaf;
 }
 
+// The walk's first node.  With the LDS tree the root's own box test is
+// skipped: the walk starts at the root's near child for the ray's octant (the
+// root's `next` link).  The root box holds every tree sphere, so skipping its
+// test only forgoes a cull (exact); a ray that starts inside
+// the scene's box -- nearly every ray -- enters it anyway (one node test per
+// walk fewer).  A one-node tree (the root a leaf) starts at the root.
+template <bool kLds>
+__device__ __forceinline__ uint32_t sphere_walk_entry(uint32_t root, uint32_t oct, uint32_t nnodes) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    if (kLds && nnodes > 1u) {
+        typedef const __attribute__((address_space(3))) char *lds_cptr;
+        return *(const __attribute__((address_space(3))) uint32_t *)((lds_cptr)(uintptr_t)root + 32 + 4u * oct) &
+               0xFFFFu;
+    }
+#endif
+    (void)oct;
+    (void)nnodes;
+    return root;
+}
+
 // The walk's per-ray slab offsets for inflation e: nlo = -((o + e) inv),
 // nhi = -((o - e) inv).
 __device__ __forceinline__ void sphere_slabs(F3 org, F3 inv, float e, F3 &nlo, F3 &nhi) {
@@ -1094,7 +1114,7 @@ void trace_kernel(TraceParams p) {
                     best_i = -1;
                     if (kBvh) {
                         spheres_big(p, org, dir, best_t, best_i);
-                        node = sph_root;
+                        node = sphere_walk_entry<kLds>(sph_root, oct, p.nnodes);
                         // (RT_AMD_ABLATE=1: timing-only diagnostic, results are wrong)
                         phase = (p.ablate & 1u) ? kTriInit : kSph;
                         if (!kMesh && bounce == 0 && (spl1 >> 16) != kSphListWalk) {
@@ -2376,7 +2396,7 @@ __device__ __forceinline__ uint32_t serial_trace_b(const TraceParams &p, const B
             F3 nlo, nhi;
             sphere_slabs(org, inv, sph_inflation(p, bnd, best_t), nlo, nhi);
             const uint32_t ooff = kLds ? 4u * oct : oct;
-            uint32_t node = sph_root;
+            uint32_t node = sphere_walk_entry<kLds>(sph_root, oct, p.nnodes);
             do {
                 uint32_t leaf;
                 if (sphere_node<kLds>(view, inv, ooff, best_t, nlo, nhi, node, leaf, cnt))
