@@ -147,14 +147,26 @@ constexpr uint32_t kBatch = 8;  // spheres per scalar-load batch (sphere count p
 // (independent of t_max) are computed for the whole batch, and the in-order
 // root/t_max updates run only when some lane's discriminant is non-negative
 // (rare; wave-uniform skip).
+// The last batch tests only the scene's spheres: a wave-uniform guard skips
+// the padding's arithmetic (world.txt's 9 spheres took 16 tests per ray;
+// RT_BRUTE_PADDED restores the padded batches).
 __device__ __forceinline__ void spheres_brute(const TraceParams &p, F3 org, F3 dir, float &best_t,
                                               int &best_i) {
     const float tmin = 0.001f;
-    for (uint32_t i0 = 0; i0 < p.nsph_padded; i0 += kBatch) {
+#ifdef RT_BRUTE_PADDED
+    const uint32_t n = p.nsph_padded;
+#else
+    const uint32_t n = p.nsph;
+#endif
+    for (uint32_t i0 = 0; i0 < n; i0 += kBatch) {
+        const uint32_t m = n - i0;  // spheres left (>= kBatch except in the last batch)
         float hb[kBatch], disc[kBatch];
         bool any = false;
 #pragma unroll
         for (uint32_t k = 0; k < kBatch; ++k) {
+            hb[k] = 0.0f;
+            disc[k] = -1.0f;
+            if (k != 0u && k >= m) continue;  // (wave-uniform)
             const float4 S = uniform_load(p.sph_hot, i0 + k);
             const float ocx = org.x - S.x, ocy = org.y - S.y, ocz = org.z - S.z;
             hb[k] = (ocx * dir.x + ocy * dir.y) + ocz * dir.z;
