@@ -676,8 +676,12 @@ int render_frame(WorldState &w, const CameraModel &cam, size_t width, size_t hei
         if (sp->mode == kRngSerialCount) chunk = env_u64("RT_AMD_SERIAL_CCHUNK", 128);
         // the pixel table pass: chunks of consecutive positions of one pixel, not
         // whole pixels (a pixel's span is 10^3 positions: whole-pixel chunks
-        // left most waves without work)
-        if (sp->mode == kRngSerialPixel) chunk = env_u64("RT_AMD_SERIAL_PCHUNK", 64);
+        // left most waves without work); 128 since round 5
+        // (profiles/round5_serial/sweep_pchunk.jsonl: 64 / 128 / 192 / 256 / 512
+        // -> world.txt 960x540x16 89.1 / 84.6 / 83.9 / 85.0 / 88.9 ms, 1920x1080x16
+        // 365 / 337 / 334 / 337 / 355 ms, RTOW at C2 settings 699 / 665 / 670 /
+        // 693 / 790 ms)
+        if (sp->mode == kRngSerialPixel) chunk = env_u64("RT_AMD_SERIAL_PCHUNK", 128);
         p.chunk = (uint32_t)std::max<uint64_t>(1, chunk);
         uint64_t parts = std::max<uint64_t>(
             1, std::min<uint64_t>({(uint64_t)(p.step ? 64 : 16), kMaxParts, njobs / (16 * chunk) + 1}));
@@ -1190,10 +1194,15 @@ static int serial_find_states(WorldState &w, const CameraModel &cam, size_t widt
         // block length: the count pass's walks use serial_walk_block(L) (256
         // blocks); the coalescing search RT_AMD_SERIAL_R samples (default 32,
         // <= kMaxWalkBlocks blocks per iteration)
+        // (the pixel table's walks: blocks of 64 samples up to 48 k-sample
+        // iterations, then about 768 blocks per iteration -- 128 samples at 64
+        // spp's 96 k: RTOW at C2 settings 665 -> 645 ms, world.txt unchanged)
+        uint64_t walk_r_def = 64;
+        while (walk_r_def < kMaxWalkR && L > walk_r_def * 768) walk_r_def *= 2;
         const uint64_t R_walk =
             coalesce ? std::min<uint64_t>(L, std::max<uint64_t>({env_u64("RT_AMD_SERIAL_R", 32), 1,
                                                                  (L + kMaxWalkBlocks - 1) / kMaxWalkBlocks}))
-            : pixtab ? std::min<uint64_t>(L, std::max<uint64_t>({env_u64("RT_AMD_SERIAL_WALKR", 64), 1,
+            : pixtab ? std::min<uint64_t>(L, std::max<uint64_t>({env_u64("RT_AMD_SERIAL_WALKR", walk_r_def), 1,
                                                                  (L + kMaxWalkBlocks - 1) / kMaxWalkBlocks}))
                      : serial_walk_block((uint32_t)L);
         // the pixel table's walks read each block's rows from LDS (as u8 counts:
