@@ -1041,7 +1041,14 @@ static int serial_find_states(WorldState &w, const CameraModel &cam, size_t widt
         // c_raytracer / RTOW / world.txt 32 -> 457 / 315 / - ms, 128 -> 418 /
         // 281 / 364, 256 -> 416 / 285 / 360, 512 -> 427 / 281 / -; z 1.2 and
         // 1.0 cost more at every EST, 1.8 and 2.1 as much or more)
-        const uint64_t est = std::max<uint64_t>(1, env_u64("RT_AMD_SERIAL_EST", 128));
+        // (round 5, with the pixel table: x2 per x4 samples per pixel from 16 spp,
+        // like the iteration length -- profiles/round5_serial/sweep_estimate_
+        // traces*.jsonl: world.txt 960x540x16 64 / 96 / 128 / 192 -> 84.7 / 84.0 /
+        // 83.2 / 84.2 ms; RTOW at C2 settings 128 / 192 / 256 / 320 / 384 -> 639 /
+        // 604 / 591 / 588 / 594 ms)
+        uint64_t est_def = 128;
+        for (uint64_t q = 64; q <= spp; q *= 4) est_def *= 2;
+        const uint64_t est = std::max<uint64_t>(1, env_u64("RT_AMD_SERIAL_EST", est_def));
         const uint64_t R = std::max<uint64_t>(
             1, std::min<uint64_t>({(est + spp - 1) / spp, 64, 0x7FFFFFFFull / N}));
         const uint64_t npix = (uint64_t)width * height;
