@@ -69,6 +69,22 @@ def main(src, dst, config="c2"):
                 out["launch"] = b.get("launch_settings")
                 out["bench_ms_per_step"] = b.get("ms_per_step")
                 out["bench_avg_launch_ms"] = (b.get("roofline") or {}).get("avg_launch_ms")
+    # the timed region's launches: bench.py's last `steps` lean trace_kernel
+    # dispatches (before them: warm-up frames, after them only counting-variant
+    # frames), their mean beside the all-dispatch average rocprof's stats give
+    traces = glob.glob(os.path.join(src, "trace", "*kernel_trace.csv"))
+    steps = None
+    if os.path.exists(logf):
+        for line in open(logf):
+            if line.startswith("{") and '"metric"' in line:
+                steps = json.loads(line).get("steps")
+    if traces and steps:
+        lean = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+                      for r in csv.DictReader(open(traces[0])) if short(r["Kernel_Name"]) == "trace_kernel")
+        timed = [d for _, d in lean[-steps:]]
+        if timed and "trace_kernel" in out["kernels"]:
+            out["kernels"]["trace_kernel"]["timed_launches"] = len(timed)
+            out["kernels"]["trace_kernel"]["timed_avg_ns"] = sum(timed) / len(timed)
     with open(os.path.join(dst, "summary.json"), "w") as fh:
         json.dump(out, fh, indent=1)
     tr = out["kernels"].get("trace_kernel", {})
