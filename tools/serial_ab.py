@@ -2,7 +2,7 @@
 mode) across library builds / env settings in ONE process.
 
   python tools/serial_ab.py --variant cur=rust-swift-raytracer_amd/lib/libraytracer.so \
-      --variant prev=ab/prev/libraytracer.so[:ENV=V...] [--cases world:960x540x16/8,...] [--rounds 3]
+      --variant prev=ab/prev/libraytracer.so[:ENV=V...][:ACCEL=bvh] [--cases world:960x540x16/8,...] [--rounds 3]
 
 Prints one JSON line per (variant, case): median wall ms of the SERIAL frame,
 the start-state search ms, iterations and iterations stopped short, and
@@ -49,21 +49,23 @@ def main():
         parts = rest.split(":")
         path = parts[0] if os.path.isabs(parts[0]) else os.path.join(ROOT, parts[0])
         env = dict(kv.split("=", 1) for kv in parts[1:])
-        variants.append((label, path, env))
+        # ACCEL=brute|bvh|auto: the frame's RtRenderOptions.accel, not an env setting
+        accel = {"auto": R.ACCEL_AUTO, "brute": R.ACCEL_BRUTE, "bvh": R.ACCEL_BVH}[env.pop("ACCEL", "auto")]
+        variants.append((label, path, env, accel))
     worlds = {}
-    for label, path, env in variants:
+    for label, path, env, _ in variants:
         for name, *_ in cases:
             worlds[(label, name)] = R.World(_scene(name), lib_path=path)
     res = {}
     ref = {}
     for rnd in range(args.rounds + 1):
         for name, w, h, spp, depth in cases:
-            for label, path, env in variants:
+            for label, path, env, accel in variants:
                 saved = {k: os.environ.get(k) for k in env}
                 os.environ.update(env)
                 world = worlds[(label, name)]
                 t = time.perf_counter()
-                img, st = world.render(w, h, spp, depth, mode=R.RNG_SERIAL)
+                img, st = world.render(w, h, spp, depth, mode=R.RNG_SERIAL, accel=accel)
                 wall = (time.perf_counter() - t) * 1e3
                 for k, v in saved.items():
                     if v is None:
