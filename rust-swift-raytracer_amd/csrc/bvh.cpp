@@ -55,7 +55,24 @@ struct Builder {
     std::vector<Node> nodes;
     uint32_t max_depth = 0;
 
-    Builder(std::vector<Prim> &p, uint32_t ls, double ph = 0) : prims(p), leaf_size(ls), phantom(ph) {}
+    // SAH bins per axis (RT_AMD_SAH_BINS for sphere trees, RT_AMD_TRI_SAH_BINS
+    // for triangle trees; 2 .. kMaxBins).  16 until round 5; A/B in one process
+    // (profiles/round5_walk/ab_*_sah_bins.jsonl): C2 lean frame 16 / 32 / 64 /
+    // 128 -> 3.754 / 3.745 / 3.712 / 3.718 ms; C5 triangle trees 16 / 32 / 64 ->
+    // 148.0 / 144.2 / 144.7 ms (C5 scene load 3.1 -> 3.7 s on 8 host threads).
+    // tools/sbvh_sim: a diffuse bounce's walk in RTOW 16.6 -> 15.8 node visits
+    // at 64 bins, its wave's longest 29.3 -> 28.6.
+    static constexpr int kMaxBins = 128;
+    int bins = 16;
+    static int env_bins(const char *name, int def) {
+        const char *e = std::getenv(name);
+        const int b = e ? std::atoi(e) : def;
+        return b >= 2 && b <= kMaxBins ? b : def;
+    }
+
+    Builder(std::vector<Prim> &p, uint32_t ls, double ph = 0)
+        : prims(p), leaf_size(ls), phantom(ph),
+          bins(ph > 0 ? env_bins("RT_AMD_TRI_SAH_BINS", 32) : env_bins("RT_AMD_SAH_BINS", 64)) {}
 
     // Subtrees of at least kParMin prims below depth kParDepth are built on
     // their own threads (they partition disjoint prim ranges) and spliced in
@@ -138,7 +155,7 @@ struct Builder {
         nodes[n].box = box;
         if (count <= leaf_size) { make_leaf(n, first, count); return; }
         // binned SAH over the centroid box (and the normal box for triangles)
-        constexpr int kBins = 16;
+        const int kBins = bins;
         double best_cost = std::numeric_limits<double>::infinity();
         int best_axis = -1, best_split = 0;
         double best_lo = 0, best_ext = 1;
@@ -147,8 +164,8 @@ struct Builder {
             const double lo = ax < 3 ? cbox.lo[ax] : nbox.lo[ax - 3];
             const double ext = (ax < 3 ? cbox.hi[ax] : nbox.hi[ax - 3]) - lo;
             if (!(ext > 0)) continue;
-            Box bb[kBins], nb[kBins];
-            uint32_t cnt[kBins] = {0};
+            Box bb[kMaxBins], nb[kMaxBins];
+            uint32_t cnt[kMaxBins] = {0};
             for (uint32_t i = first; i < first + count; ++i) {
                 int b = (int)((key(prims[i], ax) - lo) / ext * kBins);
                 b = std::min(kBins - 1, std::max(0, b));
@@ -156,8 +173,8 @@ struct Builder {
                 nb[b].grow(prims[i].n);
                 ++cnt[b];
             }
-            double left[kBins];
-            uint32_t lc[kBins];
+            double left[kMaxBins];
+            uint32_t lc[kMaxBins];
             Box acc, nacc;
             uint32_t c = 0;
             for (int b = 0; b < kBins; ++b) {
