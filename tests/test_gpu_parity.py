@@ -291,8 +291,8 @@ def test_scheduling_knobs_do_not_change_samples(monkeypatch, scene):
 @pytest.mark.parametrize("scene", ["rtow", "mesh_soup"])
 def test_tree_shape_knobs_do_not_change_samples(monkeypatch, scene):
     """Leaf sizes of the sphere, triangle and camera trees, the SAH's phantom
-    scale and the radius above which spheres stay out of the tree are
-    load-time knobs: they reshape the trees, never a
+    scale and bin counts, and the radius above which spheres stay out of the
+    tree are load-time knobs: they reshape the trees, never a
     sample (every frame equals the default build's, bit for bit)."""
     src = scene_text("rtow.txt") if scene == "rtow" else _triangle_scene(41, 400, spheres=40)
     w, h, spp = 96, 54, 4
@@ -300,6 +300,8 @@ def test_tree_shape_knobs_do_not_change_samples(monkeypatch, scene):
     for env in [dict(RT_AMD_LEAF="1"), dict(RT_AMD_LEAF="3"), dict(RT_AMD_LEAF="7"), dict(RT_AMD_TRI_LEAF="2"),
                 dict(RT_AMD_TRI_LEAF="7"), dict(RT_AMD_CAM_LEAF="1"), dict(RT_AMD_CAM_LEAF="5"),
                 dict(RT_AMD_TRI_PHANTOM="0.5"), dict(RT_AMD_BIG_K="2"),
+                dict(RT_AMD_SAH_BINS="2"), dict(RT_AMD_SAH_BINS="16"), dict(RT_AMD_TRI_SAH_BINS="4"),
+                dict(RT_AMD_TRI_SAH_BINS="128"),
                 dict(RT_AMD_BIG_K="1e9"), dict(RT_AMD_BIG_K="0"),
                 # the binary triangle walk instead of the 4-wide image (read at device init)
                 dict(RT_AMD_TRI_WIDE="0"), dict(RT_AMD_TRI_WIDE="0", RT_AMD_TRI_LEAF="3")]:
