@@ -64,6 +64,11 @@ struct Builder {
     // at 64 bins, its wave's longest 29.3 -> 28.6.
     static constexpr int kMaxBins = 128;
     int bins = 16;
+    // the binning scratch, reused by every node of this builder (the bins are
+    // done before build() recurses): off the stack, which load_world's callers
+    // may keep small (secondary threads)
+    struct BinScratch { std::vector<Box> bb, nb; std::vector<uint32_t> cnt, lc; std::vector<double> left; };
+    BinScratch scr;
     static int env_bins(const char *name, int def) {
         const char *e = std::getenv(name);
         const int b = e ? std::atoi(e) : def;
@@ -164,8 +169,13 @@ struct Builder {
             const double lo = ax < 3 ? cbox.lo[ax] : nbox.lo[ax - 3];
             const double ext = (ax < 3 ? cbox.hi[ax] : nbox.hi[ax - 3]) - lo;
             if (!(ext > 0)) continue;
-            Box bb[kMaxBins], nb[kMaxBins];
-            uint32_t cnt[kMaxBins] = {0};
+            scr.bb.assign(kBins, Box());
+            scr.nb.assign(kBins, Box());
+            scr.cnt.assign(kBins, 0u);
+            scr.left.resize(kBins);
+            scr.lc.resize(kBins);
+            Box *bb = scr.bb.data(), *nb = scr.nb.data();
+            uint32_t *cnt = scr.cnt.data();
             for (uint32_t i = first; i < first + count; ++i) {
                 int b = (int)((key(prims[i], ax) - lo) / ext * kBins);
                 b = std::min(kBins - 1, std::max(0, b));
@@ -173,8 +183,8 @@ struct Builder {
                 nb[b].grow(prims[i].n);
                 ++cnt[b];
             }
-            double left[kMaxBins];
-            uint32_t lc[kMaxBins];
+            double *left = scr.left.data();
+            uint32_t *lc = scr.lc.data();
             Box acc, nacc;
             uint32_t c = 0;
             for (int b = 0; b < kBins; ++b) {
