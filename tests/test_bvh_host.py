@@ -75,3 +75,31 @@ def test_primary_sphere_lists_cover_every_candidate(list_checker, tmp_path, w, h
     assert r.returncode == 0 and "OK" in r.stdout, r.stdout + r.stderr
     if move is None and w > 2:
         assert "candidates 0" not in r.stdout  # the frame does see tree spheres
+
+
+def test_load_world_on_a_small_thread_stack():
+    """load_world builds the trees on the caller's thread (the top levels; deeper
+    subtrees on worker threads): the SAH binning keeps its scratch off the stack,
+    so a caller's secondary thread with a small stack (Swift / GCD threads get
+    512 KB, here 192 KB) loads a 20k-triangle mesh with 60 spheres."""
+    import threading
+
+    import raytracer_amd as R
+
+    src = S.mesh(nx=100, ny=100, nspheres=60)
+    res = {}
+
+    def load():
+        try:
+            res["tris"] = R.World(src) is not None
+        except Exception as e:  # (reported below)
+            res["err"] = repr(e)
+
+    old = threading.stack_size(192 * 1024)
+    try:
+        th = threading.Thread(target=load)
+        th.start()
+        th.join(120)
+    finally:
+        threading.stack_size(old)
+    assert res.get("tris") is True, res
