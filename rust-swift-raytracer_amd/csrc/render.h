@@ -59,6 +59,10 @@ RT_HOST_DEVICE inline double serial_M(const SerialPred &m, uint32_t j) {
 }
 
 // Kernel argument block (lives in the kernarg segment -> SGPRs).
+// job-queue partitions of one launch at most (the counters are kMaxJobParts
+// u32 slots, 128 B apart, per set)
+constexpr uint32_t kMaxJobParts = 1024;
+
 struct TraceParams {
     const float4 *sph_hot;    // nsph_padded x (cx, cy, cz, r*r); pad = NaN (never hit)
     const float4 *sph_cold;   // nsph_padded x (r, material id bits, 0, 0)
@@ -77,6 +81,8 @@ struct TraceParams {
     float inv_spp;            // 1.0 / spp as f32 (common.rs:345)
     uint32_t alpha_u8;        // the alpha byte: every pixel's is the same (resolve_kernel)
     uint32_t *job_counter;    // nparts counters, 32 u32 apart; zeroed before every launch
+    uint32_t *job_counter_next;  // frames: the other set of kMaxParts counters, which this
+                                 // launch zeroes for the next one (no fill launch per frame)
     unsigned long long *stats;// nullptr, or kStatSlots per wave (wave = block * waves per
                               // block + wave in block): rays, tri in t-range, BVH sphere
                               // tests, BVH node tests, 4 stamp counters, triangle-BVH node

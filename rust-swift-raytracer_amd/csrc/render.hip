@@ -970,6 +970,10 @@ void trace_kernel(TraceParams p) {
             p.njobs = npq * E;
         }
     }
+    // frames: zero the other job-counter set for the launch after this one
+    // (stream order: it starts once this grid has finished)
+    if (!kSerial && p.job_counter_next != nullptr && blockIdx.x == 0)
+        for (uint32_t i = threadIdx.x; i < kMaxJobParts; i += blockDim.x) p.job_counter_next[32u * i] = 0u;
     const uint32_t lane = __lane_id();
     // Each section of the loop (ray setup, sphere walk, triangle setup and
     // walk, shading, the chunk resolve, the refill) re-reads the parameters it

@@ -84,7 +84,7 @@ size_t tile_row(size_t k, uint32_t row_block, uint32_t rank, uint32_t nranks) {
 }
 
 static_assert(kPrimaryTriStripW == kTriStripW, "render.h and bvh.h strip widths");
-static constexpr uint64_t kMaxParts = 1024;  // job-queue partitions (render.hip)
+static constexpr uint64_t kMaxParts = kMaxJobParts;  // job-queue partitions (render.h)
 static constexpr uint32_t kPixtabParts = 64;  // the pixel table pass's (zeroed by the window kernel)
 
 static int device_for(WorldState &w, int want, DeviceState *&out) {
@@ -242,7 +242,7 @@ static int device_for(WorldState &w, int want, DeviceState *&out) {
                 d->blocks_per_cu[c][st] = std::max(d->blocks_per_cu[c][st], 1);
                 d->blocks_per_cu_bvh[c][st] = std::max(d->blocks_per_cu_bvh[c][st], 1);
             }
-        HIP_TRY(hipMalloc((void **)&d->counter, kMaxParts * 128));
+        HIP_TRY(hipMalloc((void **)&d->counter, 2 * kMaxParts * 128));
         slot = std::move(d);
     }
     out = slot.get();
@@ -447,6 +447,10 @@ int render_frame(WorldState &w, const CameraModel &cam, size_t width, size_t hei
     p.mats = d->mats;
     p.samples = d->samples;
     p.job_counter = d->counter;
+    p.job_counter_next = nullptr;
+    // (set 0 is also the SERIAL passes' scratch: the double-buffered frame sets
+    // start over from a fill after them)
+    if (sp) d->cset_clean[0] = d->cset_clean[1] = false;
     p.replay = d_replay ? d_replay : d->replay;
     const Vec3 cv[4] = {cam.origin, cam.lower_left, cam.horizontal, cam.vertical};
     for (int i = 0; i < 4; ++i) { p.cam[3 * i] = cv[i].x; p.cam[3 * i + 1] = cv[i].y; p.cam[3 * i + 2] = cv[i].z; }
@@ -789,8 +793,20 @@ int render_frame(WorldState &w, const CameraModel &cam, size_t width, size_t hei
                 p.ring = d->ring;
             }
             p.nparts = (uint32_t)parts;
-            HIP_TRY(hipMemsetAsync(d->counter, 0, parts * 128, s));
+            // two counter sets: this launch takes set cset (zeroed by the launch
+            // before it, or filled here) and zeroes the other for the next one,
+            // so back-to-back frames need no fill launch (a fill plus its gap
+            // before the trace kernel was ~20 us of every C2 frame)
+            uint32_t *const cur = d->counter + (size_t)d->cset * kMaxParts * 32;
+            if (!d->cset_clean[d->cset]) HIP_TRY(hipMemsetAsync(cur, 0, parts * 128, s));
+            p.job_counter = cur;
+            p.job_counter_next = d->counter + (size_t)(d->cset ^ 1u) * kMaxParts * 32;
             HIP_TRY(launch_trace(p, (uint32_t)blocks, s));
+            d->cset_clean[d->cset] = false;
+            d->cset ^= 1u;
+            d->cset_clean[d->cset] = true;
+            p.job_counter = d->counter;
+            p.job_counter_next = nullptr;
             lean_plan = ctv == 0 ? lp : plan(0, njobs);
             d->last_jobs = fused ? 0 : njobs;
             d->last_spp = spp;
@@ -1549,7 +1565,7 @@ int render_frame_multi(WorldState &w, const CameraModel &cam, size_t width, size
         rc = device_for(w, devs[g], ds[g]);
         if (rc) return rc;
         ss[g] = (g == 0 && stream) ? stream : ds[g]->stream;
-        HIP_TRY(grow(ds[g]->tile, ds[g]->tile_cap, max_rows * width));
+        if (n > 1) HIP_TRY(grow(ds[g]->tile, ds[g]->tile_cap, max_rows * width));
     }
     if (n > 1) {
         HIP_TRY(hipSetDevice(devs[0]));
@@ -1602,8 +1618,9 @@ int render_frame_multi(WorldState &w, const CameraModel &cam, size_t width, size
         }
         RtRenderStats sg;
         HIP_TRY(hipSetDevice(devs[g]));
-        rc = render_frame(w, cam, width, height, og, ds[g]->tile, ss[g], stats ? &sg : nullptr, nullptr,
-                          serial ? ds[g]->sstates : nullptr, /*defer_stats=*/true);
+        // (one device: its tile is the frame, rendered in place -- no gather)
+        rc = render_frame(w, cam, width, height, og, n == 1 ? d_out : ds[g]->tile, ss[g], stats ? &sg : nullptr,
+                          nullptr, serial ? ds[g]->sstates : nullptr, /*defer_stats=*/true);
         if (rc) return rc;
     }
     for (uint32_t g = 0; g < n && stats; ++g) {
@@ -1632,10 +1649,11 @@ int render_frame_multi(WorldState &w, const CameraModel &cam, size_t width, size
         }
     }
     // RCCL gather of equal-size tiles to the first device (over xGMI); with one
-    // device the tile is the frame and the gather lands in d_out directly
+    // device the tile was rendered into d_out (until round 5 a one-rank gather
+    // copied it there: one RCCL kernel and ~17 us per frame)
     const size_t bytes = max_rows * width * 4;
-    NCCL_TRY(ncclGroupStart());
-    for (uint32_t g = 0; g < n; ++g) {
+    if (n > 1) NCCL_TRY(ncclGroupStart());
+    for (uint32_t g = 0; g < n && n > 1; ++g) {
         const ncclResult_t r = ncclGather(ds[g]->tile, n > 1 ? (void *)ds[0]->gath : (void *)d_out, bytes,
                                           ncclUint8, 0, (*comms)[g], ss[g]);
         if (r != ncclSuccess) {
@@ -1644,7 +1662,7 @@ int render_frame_multi(WorldState &w, const CameraModel &cam, size_t width, size
             return -4;
         }
     }
-    NCCL_TRY(ncclGroupEnd());
+    if (n > 1) NCCL_TRY(ncclGroupEnd());
     HIP_TRY(hipSetDevice(devs[0]));
     if (n > 1)
         HIP_TRY(launch_assemble(ds[0]->gath, d_out, (uint32_t)width, (uint32_t)height, B, n,

@@ -95,7 +95,9 @@ struct DeviceState {
     uint32_t *sjump = nullptr;
     uint32_t *sctrl = nullptr;
     unsigned long long *scheck = nullptr;                       // chain-check count
-    uint32_t *counter = nullptr;                                // job counter
+    uint32_t *counter = nullptr;                                // job counters: 2 sets of kMaxParts
+    uint32_t cset = 0;              // the set the next frame launch uses ...
+    bool cset_clean[2] = {false, false};  // ... and whether each set is known to be zero
     unsigned long long *stats = nullptr; size_t stats_cap = 0;  // per-wave counter records
     // resident workgroups per CU of each kernel variant, [0]: whole walks, [1]: sliced walks
     // [count][step]: workgroups per CU of each kernel instance
