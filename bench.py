@@ -62,6 +62,15 @@ def algorithmic_flops(st):
             + 40 * st["rays"] + 20 * st["samples"])
 
 
+def s8d_literal_flops(st):
+    """SURVEY.md 8(d)'s price list taken literally on the executed work: no
+    price for BVH box tests (the list has none), sphere and triangle tests as
+    executed."""
+    sph = st["bvh_sphere_tests"] + st["big_sphere_tests"]
+    return (17 * sph + 14 * st["bvh_tri_tests"] + 60 * st["tri_in_range"] + 40 * st["rays"]
+            + 20 * st["samples"])
+
+
 def executed_flops(st):
     """The same price list applied to the work the kernel actually executed:
     sphere tests done (BVH leaves + spheres kept out of the tree, or all of
@@ -223,7 +232,8 @@ def _timed(args, step, stream, sync, barrier):
     elapsed = time.perf_counter() - t0
     stats = [step(True) for _ in range(max(1, min(args.steps, 3)))]
     assert all(s["rays"] == st_warm["rays"] for s in stats), "frames must be identical"
-    # (a timed frame is one job-counter fill + the trace launches)
+    # (a timed frame's render is its trace launch(es): each launch zeroes the
+    # other job-counter set for the next one, so no fill launch per frame)
     trace_ms = (sum(a.elapsed_time(b) for a, b in evs) / args.steps
                 / max(1, stats[-1]["trace_launches"]))
     count_trace_ms = sum(s["trace_ms"] for s in stats) / max(1, sum(s["trace_launches"] for s in stats))
@@ -356,8 +366,11 @@ def single_process(args):
     st_warm, st0, elapsed, trace_ms, count_trace_ms = _timed(args, step, stream, sync, lambda: None)
     moved = _post_move(world, step, sync)
     rows = R.tile_rows(H, ROW_BLOCK, 0, ngpu) if ngpu > 1 else H
-    par = (f"row-tiles x{ngpu} (block {ROW_BLOCK}), one process, RCCL ncclGather "
-           f"({ranks} ranks) to device 0")
+    if ngpu > 1:
+        par = (f"row-tiles x{ngpu} (block {ROW_BLOCK}), one process, RCCL ncclGather "
+               f"({ranks} ranks) to device 0 + assemble kernel")
+    else:
+        par = "one device renders the frame in place (no RCCL call)"
     extra = {"rccl_ranks": ranks, "launch": "single process", "post_move": moved}
     if ngpu == 1 and not args.no_serial:
         torch.cuda.set_stream(torch.cuda.default_stream(dev))
@@ -391,6 +404,10 @@ def multi_process(args, world_size):
     dev = torch.device("cuda", local_rank)
     tile = torch.zeros(max_rows * W * 4, dtype=torch.uint8, device=dev)
     gathered = torch.empty(nr * max_rows * W * 4, dtype=torch.uint8, device=dev) if nr > 1 else None
+    # rank 0 assembles the frame from the gathered tiles inside every step (the
+    # single-process launch's assemble_kernel after its ncclGather): both launch
+    # shapes time the same work
+    frame = torch.zeros(H * W * 4, dtype=torch.uint8, device=dev) if nr > 1 and rank == 0 else None
     # one explicit stream for the frames, their HIP events and the RCCL
     # gather (the default stream's handle is 0, which the library would
     # replace with its own stream)
@@ -413,6 +430,9 @@ def multi_process(args, world_size):
                 tiles.gather(tile, gathered)  # RCCL all-gather over xGMI
             else:
                 gathered.copy_(tiles.gather_any(tile.cpu(), nr))
+            if frame is not None:
+                R.assemble_tiles(gathered.data_ptr(), frame.data_ptr(), W, H, ROW_BLOCK, nr, max_rows,
+                                 stream.cuda_stream)
         return st
 
     barrier = dist.barrier if nr > 1 else (lambda: None)
@@ -427,14 +447,20 @@ def multi_process(args, world_size):
         dist.all_reduce(t_sum, op=dist.ReduceOp.SUM)
         elapsed, rays = float(t_max[0]), int(t_sum[0])
         if os.environ.get("RT_BENCH_VERIFY") == "1":
-            # the assembled frame must equal a one-rank render (rehearsal check)
+            # the frame the last timed step assembled on rank 0 (and the host
+            # reassembly of the gathered tiles) must equal a one-rank render
             img = tiles.assemble(gathered.cpu().numpy(), W, H, ROW_BLOCK, nr)
             if rank == 0:
                 ref, _ = world.render(W, H, spp, depth, device=local_rank)
                 assert (img == ref).all(), "assembled multi-rank frame differs"
+                timed = frame.cpu().numpy().reshape(H, W, 4)
+                assert (timed == ref).all(), "timed-step frame differs from the one-rank frame"
                 print("verify: assembled frame == single-rank frame", file=sys.stderr)
+                print("verify: timed-step frame == single-rank frame", file=sys.stderr)
     if rank == 0:
-        par = f"row-tiles x{nr} (block {ROW_BLOCK}), one process per GPU, RCCL all-gather"
+        par = (f"row-tiles x{nr} (block {ROW_BLOCK}), one process per GPU, RCCL all-gather "
+               "+ assemble kernel on rank 0" if nr > 1 else
+               "one device renders the frame in place (no RCCL call)")
         _report(args, src, world, W, H, spp, depth, st0, rays, elapsed, trace_ms, count_trace_ms,
                 nr, rows, par, {"rccl_ranks": nr, "launch": "torch.distributed.run"})
     if nr > 1:
@@ -457,7 +483,7 @@ def _report(args, src, world, W, H, spp, depth, st0, rays, elapsed, trace_ms, co
     # the timed (uncounted) kernel's schedule: profiles record it with their
     # counters, and the traffic below counts only if it is the same
     launch = {k[len("launch_"):]: st0[k] for k in LAUNCH_KEYS}
-    traffic, tsrc = None, None
+    traffic, tsrc, ent = None, None, {}
     tfile = os.path.join(ROOT, "profiles", "hbm_traffic.json")
     if os.path.exists(tfile):
         with open(tfile) as fh:
@@ -478,6 +504,35 @@ def _report(args, src, world, W, H, spp, depth, st0, rays, elapsed, trace_ms, co
                 "profiled_lib_sha256": ent.get("lib_sha256"), "benched_lib_sha256": loaded,
                 "same_binary": ent.get("lib_sha256") == loaded}
     ms_per_step = elapsed / args.steps * 1e3
+    # VALU evidence of the same hash-keyed profile (tools/pmc_summary.py): lanes
+    # active per VALU instruction, VALU lane-slots per ray and the issue rate
+    # against the v_add_f32 microbenchmark (tools/ubench_valu on the box,
+    # profiles/valu_ceiling.json) -- null unless the profiled trace kernel is
+    # the one this run loaded
+    same = bool(tsrc and tsrc["same_trace_kernel"])
+    pv = (ent.get("valu") or {}) if same else {}
+    ceiling = None
+    cfile = os.path.join(ROOT, "profiles", "valu_ceiling.json")
+    if os.path.exists(cfile):
+        with open(cfile) as fh:
+            ceiling = json.load(fh)
+    no_fma = ceiling["v_add_f32_tera_lane_ops_per_s"] if ceiling else None
+    s8d_tflops = s8d_literal_flops(st0) / launches / (trace_ms * 1e-3) / 1e12
+    valu = {"valu_issue_frac": pv.get("issue_frac_of_v_add_rate"),
+            "lanes_active": pv.get("lanes_active"),
+            "valu_lane_slots_per_ray": pv.get("lane_slots_per_ray"),
+            "wait_frac": pv.get("wait_frac"),
+            "valu_from": ent.get("from") if same else None,
+            "profile_ms_per_step": ent.get("profile_ms_per_step") if same else None,
+            "profile_timed_avg_launch_ms": ent.get("timed_avg_launch_ms") if same else None,
+            # the practical ceiling without FMA (parity forbids contraction): one
+            # f32 op per lane per v_add_f32 issue slot, measured on the box
+            "no_fma_ceiling_tflops": no_fma,
+            "frac_of_no_fma_ceiling": achieved_tflops / no_fma if no_fma else None,
+            "no_fma_ceiling_from": ceiling.get("from") if ceiling else None,
+            # SURVEY 8(d) literally: no price for box tests
+            "s8d_literal_tflops": s8d_tflops,
+            "s8d_literal_frac": s8d_tflops / FP32_VECTOR_PEAK_TFLOPS}
     result = {
         "metric": METRIC,
         "value": rays / elapsed / 1e6,
@@ -506,7 +561,7 @@ def _report(args, src, world, W, H, spp, depth, st0, rays, elapsed, trace_ms, co
                      "flops_per_launch": flops_per_launch, "flops": "executed work",
                      "brute_force_equivalent_tflops": alg_tflops,
                      "algorithmic_hbm_gbs": out_bytes / (trace_ms * 1e-3) / 1e9,
-                     "hbm_peak_gbs": HBM_PEAK_GBS},
+                     "hbm_peak_gbs": HBM_PEAK_GBS, **valu},
         "launch_settings": launch,
         "rays_per_frame": st0["rays"],
         "accel": {1: "brute", 2: "bvh"}.get(st0["accel"], "?"),

@@ -74,16 +74,26 @@ __device__ __forceinline__ F3 unit(F3 a) {  // NVec3::new, maths.rs:111-118
     return F3{a.x / len, a.y / len, a.z / len};
 }
 
-// xorshift32 (random.rs:22-30) and `x as f32 / u32::MAX as f32` == x * 2^-32.
-__device__ __forceinline__ float draw01(uint32_t &s) {
+// xorshift32 (random.rs:22-30); `x as f32 / u32::MAX as f32` == RN(x) * 2^-32.
+__device__ __forceinline__ uint32_t xorshift(uint32_t &s) {
     uint32_t x = s;
     x ^= x << 13;
     x ^= x >> 17;
     x ^= x << 5;
     s = x;
-    return (float)x * 0x1p-32f;
+    return x;
 }
-__device__ __forceinline__ float draw11(uint32_t &s) { return draw01(s) * 2.0f - 1.0f; }
+// `random_f32() * 2.0 - 1.0` (common.rs:32-38, random.rs:27-30): RN(RN(x) 2^-32 2
+// - 1) with an exact product (a power-of-two scaling of RN(x), >= 2^-31), so
+// one fma gives the same bits.
+__device__ __forceinline__ float draw11(uint32_t &s) {
+    return __builtin_fmaf((float)xorshift(s), 0x1p-31f, -1.0f);
+}
+// `n + random_f32()` (camera u, v numerators, common.rs:335-336): the same
+// exact product, one rounding
+__device__ __forceinline__ float draw_plus(uint32_t &s, float n) {
+    return __builtin_fmaf((float)xorshift(s), 0x1p-32f, n);
+}
 // common.rs:32-38 -- three draws x, y, z, normalised (no rejection sampling).
 __device__ __forceinline__ F3 draw_unit(uint32_t &s) {
     float x = draw11(s);
@@ -253,7 +263,8 @@ __device__ __forceinline__ float slab_rcp(float d) {
 struct SphBound { float A, e_abs; };  // per-ray inputs of the inflation
 __device__ __forceinline__ SphBound sph_bound(const TraceParams &p, F3 org) {
     const float ax = org.x - p.bvh_c[0], ay = org.y - p.bvh_c[1], az = org.z - p.bvh_c[2];
-    return SphBound{xsqrt((ax * ax + ay * ay) + az * az) * 1.00001f + p.bvh_r,
+    // (v_sqrt_f32, <= 1 ulp: the 1e-5 factor covers it; A is only a bound)
+    return SphBound{__builtin_amdgcn_sqrtf((ax * ax + ay * ay) + az * az) * 1.00001f + p.bvh_r,
                     2e-6f * ((fabsf(org.x) + fabsf(org.y)) + fabsf(org.z) + p.bvh_mag)};
 }
 constexpr float kErrKq = 40.5f * 0x1p-24f;  // 2.7 x 15u
@@ -1593,8 +1604,8 @@ void trace_kernel(TraceParams p) {
                 // common.rs:335-337: u drawn before v; camera.rs:84-89
                 // numerators are in [2^-32, 2^24]: exactdiv.h with the host's
                 // reciprocals whenever the denominators are in range
-                const float un = (float)col + draw01(rng);
-                const float vn = (float)row + draw01(rng);
+                const float un = draw_plus(rng, (float)col);
+                const float vn = draw_plus(rng, (float)row);
 #ifndef RT_NO_XDIV
                 const bool xd = pc.xdiv_uv != 0;
 #else
@@ -2393,8 +2404,8 @@ __device__ __forceinline__ uint32_t serial_trace_b(const TraceParams &p, const B
     const uint32_t pix = fdiv(j, p.div_sspp);
     const uint32_t row = fdiv(pix, p.div_width);
     const uint32_t col = pix - row * p.width;
-    const float un = (float)col + draw01(rng);  // camera.rs:84-89 via common.rs:335-337
-    const float vn = (float)row + draw01(rng);
+    const float un = draw_plus(rng, (float)col);  // camera.rs:84-89 via common.rs:335-337
+    const float vn = draw_plus(rng, (float)row);
 #ifndef RT_NO_XDIV
     const bool xd = p.xdiv_uv != 0;
 #else

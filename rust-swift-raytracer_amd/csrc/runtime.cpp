@@ -211,6 +211,13 @@ static int device_for(WorldState &w, int want, DeviceState *&out) {
                     tri = trace_mesh_kind(w.packed.ntri > 0, !w.tbvh.nodes.empty());
                     HIP_TRY(occupancy_global());
                     HIP_TRY(occupancy_lds(fits));
+                    if (!fits) {
+                        // the tree itself does not fit: give up the LDS tree, not
+                        // the wide triangle walk (its stacks fit without the tree)
+                        wide = true;
+                        tri = 3;
+                        HIP_TRY(occupancy_global());
+                    }
                 }
                 if (fits) d->lds_bytes = lds;
             }
@@ -1623,31 +1630,6 @@ int render_frame_multi(WorldState &w, const CameraModel &cam, size_t width, size
                           nullptr, serial ? ds[g]->sstates : nullptr, /*defer_stats=*/true);
         if (rc) return rc;
     }
-    for (uint32_t g = 0; g < n && stats; ++g) {
-        RtRenderStats sg;
-        std::memset(&sg, 0, sizeof(sg));
-        rc = collect_frame_stats(ds[g], &sg);
-        if (rc) return rc;
-        {
-            stats->samples += sg.samples; stats->rays += sg.rays;
-            stats->sphere_tests += sg.sphere_tests; stats->tri_tests += sg.tri_tests;
-            stats->tri_in_range += sg.tri_in_range;
-            stats->trace_ms = std::max(stats->trace_ms, sg.trace_ms);
-            stats->resolve_ms = std::max(stats->resolve_ms, sg.resolve_ms);
-            stats->trace_launches = std::max(stats->trace_launches, sg.trace_launches);
-            stats->waves += sg.waves; stats->accel = sg.accel;
-            stats->bvh_sphere_tests += sg.bvh_sphere_tests; stats->bvh_node_tests += sg.bvh_node_tests;
-            stats->big_sphere_tests += sg.big_sphere_tests;
-            for (int k = 0; k < 4; ++k) stats->stamp_cycles[k] += sg.stamp_cycles[k];
-            stats->tri_node_tests += sg.tri_node_tests; stats->bvh_tri_tests += sg.bvh_tri_tests;
-            stats->tri_bvh = sg.tri_bvh; stats->fused_resolve = sg.fused_resolve;
-            stats->primary_lists = sg.primary_lists; stats->camera_tree = sg.camera_tree;
-            stats->launch_parts = sg.launch_parts; stats->launch_chunk = sg.launch_chunk;
-            stats->launch_refill_min = sg.launch_refill_min; stats->launch_walk_min = sg.launch_walk_min;
-            stats->launch_tri_walk_min = sg.launch_tri_walk_min; stats->launch_wsteps = sg.launch_wsteps;
-            stats->launch_block_threads = sg.launch_block_threads; stats->launch_blocks = sg.launch_blocks;
-        }
-    }
     // RCCL gather of equal-size tiles to the first device (over xGMI); with one
     // device the tile was rendered into d_out (until round 5 a one-rank gather
     // copied it there: one RCCL kernel and ~17 us per frame)
@@ -1672,6 +1654,34 @@ int render_frame_multi(WorldState &w, const CameraModel &cam, size_t width, size
         HIP_TRY(hipSetDevice(devs[g]));
         HIP_TRY(hipEventRecord(ds[g]->done, ss[g]));
         ds[g]->done_stream = ss[g];
+    }
+    // the counted tiles' counters, collected only now: every device's tile, the
+    // gather and the assembly are enqueued before the host waits on any of them
+    for (uint32_t g = 0; g < n && stats; ++g) {
+        HIP_TRY(hipSetDevice(devs[g]));
+        RtRenderStats sg;
+        std::memset(&sg, 0, sizeof(sg));
+        rc = collect_frame_stats(ds[g], &sg);
+        if (rc) return rc;
+        {
+            stats->samples += sg.samples; stats->rays += sg.rays;
+            stats->sphere_tests += sg.sphere_tests; stats->tri_tests += sg.tri_tests;
+            stats->tri_in_range += sg.tri_in_range;
+            stats->trace_ms = std::max(stats->trace_ms, sg.trace_ms);
+            stats->resolve_ms = std::max(stats->resolve_ms, sg.resolve_ms);
+            stats->trace_launches = std::max(stats->trace_launches, sg.trace_launches);
+            stats->waves += sg.waves; stats->accel = sg.accel;
+            stats->bvh_sphere_tests += sg.bvh_sphere_tests; stats->bvh_node_tests += sg.bvh_node_tests;
+            stats->big_sphere_tests += sg.big_sphere_tests;
+            for (int k = 0; k < 4; ++k) stats->stamp_cycles[k] += sg.stamp_cycles[k];
+            stats->tri_node_tests += sg.tri_node_tests; stats->bvh_tri_tests += sg.bvh_tri_tests;
+            stats->tri_bvh = sg.tri_bvh; stats->fused_resolve = sg.fused_resolve;
+            stats->primary_lists = sg.primary_lists; stats->camera_tree = sg.camera_tree;
+            stats->launch_parts = sg.launch_parts; stats->launch_chunk = sg.launch_chunk;
+            stats->launch_refill_min = sg.launch_refill_min; stats->launch_walk_min = sg.launch_walk_min;
+            stats->launch_tri_walk_min = sg.launch_tri_walk_min; stats->launch_wsteps = sg.launch_wsteps;
+            stats->launch_block_threads = sg.launch_block_threads; stats->launch_blocks = sg.launch_blocks;
+        }
     }
     HIP_TRY(hipSetDevice(devs[0]));
     if (stats) {

@@ -124,6 +124,9 @@ def test_bench_torchrun_two_ranks_rehearsal():
                        env=env, capture_output=True, text=True, timeout=110)
     assert r.returncode == 0, r.stderr[-3000:]
     assert "verify: assembled frame == single-rank frame" in r.stderr
+    # the frame rank 0 assembled inside its timed steps (rt_assemble_tiles on the
+    # gathered tiles, as the single-process launch does after its ncclGather)
+    assert "verify: timed-step frame == single-rank frame" in r.stderr
     line = json.loads(r.stdout.strip().splitlines()[-1])
     assert line["n_gpus"] == 2 and line["rccl_ranks"] == 2
 

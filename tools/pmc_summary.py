@@ -62,29 +62,63 @@ def main(src, dst, config="c2"):
     # the bench line of the kernel-trace pass: the profiled run's schedule
     # (launch settings) and its timing, kept with the counters
     logf = os.path.join(src, "trace.log")
+    bline = None
     if os.path.exists(logf):
         for line in open(logf):
             if line.startswith("{") and '"metric"' in line:
-                b = json.loads(line)
-                out["launch"] = b.get("launch_settings")
-                out["bench_ms_per_step"] = b.get("ms_per_step")
-                out["bench_avg_launch_ms"] = (b.get("roofline") or {}).get("avg_launch_ms")
+                bline = json.loads(line)
+    if bline:
+        out["launch"] = bline.get("launch_settings")
+        out["bench_ms_per_step"] = bline.get("ms_per_step")
+        out["bench_avg_launch_ms"] = (bline.get("roofline") or {}).get("avg_launch_ms")
+        out["rays_per_frame"] = bline.get("rays_per_frame")
     # the timed region's launches: bench.py's last `steps` lean trace_kernel
-    # dispatches (before them: warm-up frames, after them only counting-variant
-    # frames), their mean beside the all-dispatch average rocprof's stats give
+    # dispatches of the frame's grid (before them: warm-up frames, after them
+    # only counting-variant frames), their mean beside the all-dispatch average
+    # rocprof's stats give.  Only valid when the bench skipped its SERIAL legs
+    # (--no-serial, as tools/profile.sh runs it): their REPLAY frames are lean
+    # trace_kernel dispatches too, after the timed region.
     traces = glob.glob(os.path.join(src, "trace", "*kernel_trace.csv"))
-    steps = None
-    if os.path.exists(logf):
-        for line in open(logf):
-            if line.startswith("{") and '"metric"' in line:
-                steps = json.loads(line).get("steps")
+    steps = bline.get("steps") if bline else None
+    if bline and "serial" in bline:
+        print("pmc_summary: the profiled bench ran its SERIAL legs; timed_avg_ns not computed "
+              "(run bench.py with --no-serial)", file=sys.stderr)
+        steps = None
     if traces and steps:
+        ls = (bline or {}).get("launch_settings") or {}
+        grid = ls.get("blocks", 0) * ls.get("block_threads", 0)
+
+        def frame_grid(r):
+            g = r.get("Grid_Size_X") or r.get("Grid_Size")
+            return not grid or g is None or int(g) == grid
+
         lean = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
-                      for r in csv.DictReader(open(traces[0])) if short(r["Kernel_Name"]) == "trace_kernel")
+                      for r in csv.DictReader(open(traces[0]))
+                      if short(r["Kernel_Name"]) == "trace_kernel" and frame_grid(r))
         timed = [d for _, d in lean[-steps:]]
         if timed and "trace_kernel" in out["kernels"]:
             out["kernels"]["trace_kernel"]["timed_launches"] = len(timed)
             out["kernels"]["trace_kernel"]["timed_avg_ns"] = sum(timed) / len(timed)
+    # VALU evidence of the timed (lean) kernel: lanes active per VALU
+    # instruction, VALU lane-slots per ray, and the issue rate against the
+    # v_add_f32 microbenchmark (profiles/valu_ceiling.json, tools/ubench_valu)
+    tk = out["kernels"].get("trace_kernel", {})
+    if "SQ_INSTS_VALU" in tk and "SQ_THREAD_CYCLES_VALU" in tk:
+        v = {"insts_valu": tk["SQ_INSTS_VALU"],
+             "lanes_active": tk["SQ_THREAD_CYCLES_VALU"] / (64.0 * tk["SQ_INSTS_VALU"])}
+        rays = out.get("rays_per_frame")
+        if rays:
+            v["lane_slots_per_ray"] = tk["SQ_INSTS_VALU"] * 64.0 / rays
+        t_ns = tk.get("timed_avg_ns") or tk.get("avg_ns")
+        if t_ns:
+            v["issue_wave_insts_per_s"] = tk["SQ_INSTS_VALU"] / (t_ns * 1e-9)
+            cf = os.path.join(os.path.dirname(dst.rstrip("/")), "valu_ceiling.json")
+            if os.path.exists(cf):
+                ceil = json.load(open(cf))["v_add_f32_wave_insts_per_s"]
+                v["issue_frac_of_v_add_rate"] = v["issue_wave_insts_per_s"] / ceil
+        if "SQ_WAIT_ANY" in tk and "SQ_WAVE_CYCLES" in tk:
+            v["wait_frac"] = tk["SQ_WAIT_ANY"] / tk["SQ_WAVE_CYCLES"]
+        out["valu"] = v
     with open(os.path.join(dst, "summary.json"), "w") as fh:
         json.dump(out, fh, indent=1)
     tr = out["kernels"].get("trace_kernel", {})
@@ -95,7 +129,10 @@ def main(src, dst, config="c2"):
                         "from": os.path.relpath(dst, os.path.dirname(path)),
                         "lib_sha256": out.get("lib_sha256"),
                         "trace_kernel_sha256": out.get("kernel_sha256"),
-                        "launch": out.get("launch")}
+                        "launch": out.get("launch"),
+                        "profile_ms_per_step": out.get("bench_ms_per_step"),
+                        "timed_avg_launch_ms": (tr.get("timed_avg_ns") or 0) * 1e-6 or None,
+                        "valu": out.get("valu")}
         with open(path, "w") as fh:
             json.dump(allc, fh, indent=1)
     print(json.dumps(out, indent=1))
