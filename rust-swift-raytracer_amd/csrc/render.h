@@ -168,6 +168,8 @@ struct TraceParams {
     FastDiv div_sspp;         // ... and its divider
     uint32_t max_draws;       // 2 + 3 * max(depth, 0): bound of the draw count search
     uint32_t sL, sK;          // kRngSerialPixel: the iteration length and the launch's K
+    const uint2 *spix;        // kRngSerialPixel (optional): per local pixel its positions
+                              // {plo, phi} (serial_window_kernel), one load per refill
     // frames of one rank whose global job indices (row * W + col) * spp + s
     // fit 32 bits (gj32 != 0): the global job of launch job j in local row q is
     // j + gj_c0 - q * gj_2p (mod 2^32), gj_c0 = (H - 1 - slab_row0) W spp,
@@ -244,7 +246,7 @@ constexpr uint32_t kSerialJumpWords = 32 * (64 + kSerialJumpT1 + 256);
 hipError_t launch_serial_window(uint32_t *ctrl, const uint32_t *jump, uint32_t *win, uint32_t n,
                                 SerialPred M, uint32_t *lo, uint32_t L, uint32_t K, uint32_t depth,
                                 uint32_t nserial, uint32_t pix_spp, uint32_t pix_emax, uint32_t *counters,
-                                uint32_t ncounters, hipStream_t stream);
+                                uint32_t ncounters, uint2 *spix, uint32_t pix_chunk, hipStream_t stream);
 // The pixel table pass's result (ptab: b of local pixel q at position plo(q) + e
 // = ptab[q * ctrl[7] + e]) gathered into the count table of the iteration
 // (table[jl * K + k], the layout the walks read; -1 outside the traced span)

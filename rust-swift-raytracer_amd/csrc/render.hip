@@ -142,6 +142,16 @@ __device__ __forceinline__ uint32_t uniform_load_u32(const uint32_t *base, uint3
 #endif
 }
 
+__device__ __forceinline__ uint2 uniform_load_u2(const uint2 *base, uint32_t i) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    typedef const __attribute__((address_space(4))) uint32_t *cu32_ptr;
+    const cu32_ptr q = (cu32_ptr)(const void *)base + 2u * i;
+    return make_uint2(q[0], q[1]);
+#else
+    return base[i];
+#endif
+}
+
 __device__ __forceinline__ uint32_t fdiv(uint32_t n, const FastDiv &f) { return fastdiv_apply(n, f); }
 
 constexpr uint32_t kWave = 64;
@@ -682,6 +692,12 @@ __device__ __forceinline__ void job_pixel(const TraceParams &p, uint32_t job, ui
 // jf / jz its first / last sample in the iteration
 __device__ __forceinline__ void serial_pixel_span(const TraceParams &p, uint32_t q, uint32_t &plo,
                                                   uint32_t &phi) {
+    if (p.spix != nullptr) {  // tabulated by the window kernel: one load
+        const uint2 s = p.spix[q];
+        plo = s.x;
+        phi = s.y;
+        return;
+    }
     const uint32_t a = p.cbase, ss = p.sspp;
     const uint32_t ln = min(p.sL, p.nserial - a);
     const uint32_t p0 = fdiv(a, p.div_sspp);
@@ -1527,7 +1543,9 @@ void trace_kernel(TraceParams p) {
         // kTraceRing slots waiting on unfinished samples the lanes stay idle)
         if (refill && !exhausted && !(fused && rfree == 0 && pool_next >= pool_end)) {
             const TraceParams &pc = kargs();  // (the refill's parameters: see kargs)
-            if (pool_next >= pool_end) {
+            // (a wave-uniform loop only in the pixel table pass, which skips
+            // chunks that hold no position of its pixel's span)
+            while (pool_next >= pool_end) {
                 uint32_t base = 0;
                 if (lane == 0) {
                     base = pbegin + (prefetch_pending ? prefetch
@@ -1550,9 +1568,22 @@ void trace_kernel(TraceParams p) {
 #ifdef RT_WAVE_TIMES
                     wt_exh = __builtin_amdgcn_s_memrealtime();
 #endif
+                    break;
                 } else {
                     pool_next = base;
                     pool_end = min(base + pc.chunk, pend);
+                    if (kSerial && pc.mode == kRngSerialPixel && pc.spix != nullptr) {
+                        // pixel rows are padded to whole chunks (the row stride E
+                        // is a multiple of the chunk: serial_window_kernel), so a
+                        // chunk lies in one pixel's row: hand out only its
+                        // positions inside the pixel's span (the rest would leave
+                        // lanes idle, serial_pixel_job) and skip chunks past it
+                        const uint32_t q = fdiv(base, pc.div_spp);
+                        const uint2 sq = uniform_load_u2(pc.spix, q);
+                        const uint32_t live_end = q * pc.spp + (sq.y >= sq.x ? sq.y - sq.x + 1u : 0u);
+                        pool_end = min(pool_end, live_end);
+                        if (pool_next >= pool_end) continue;
+                    }
 #ifdef RT_WAVE_TIMES
                     wt_pull = __builtin_amdgcn_s_memrealtime();
                     wt_jobs_tail = pool_end - pool_next;
@@ -1567,7 +1598,7 @@ void trace_kernel(TraceParams p) {
                     }
                 }
             }
-            const uint32_t avail = pool_end - pool_next;
+            const uint32_t avail = exhausted ? 0u : pool_end - pool_next;
             const uint32_t rank = __builtin_amdgcn_mbcnt_hi(
                 (uint32_t)(dead >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)dead, 0u));
             if (!active && rank < avail) {
@@ -1904,7 +1935,8 @@ __global__ __launch_bounds__(256) void serial_window_kernel(uint32_t *__restrict
                                                             SerialPred M, uint32_t *__restrict__ lo,
                                                             uint32_t L, uint32_t Kmax, uint32_t depth,
                                                             uint32_t nserial, uint32_t pix_spp, uint32_t pix_emax,
-                                                            uint32_t *__restrict__ counters, uint32_t ncounters) {
+                                                            uint32_t *__restrict__ counters, uint32_t ncounters,
+                                                            uint2 *__restrict__ spix, uint32_t pix_chunk) {
     if (ctrl[0] != 0u) return;
     // the following trace pass's job counters (instead of a fill launch)
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < ncounters; i += gridDim.x * blockDim.x)
@@ -1928,9 +1960,13 @@ __global__ __launch_bounds__(256) void serial_window_kernel(uint32_t *__restrict
                 const uint32_t lz = serial_lo(M, a, jz, K, depth, nserial);
                 const uint32_t hi = 2u * jz + 3u * (lz + K - 1u), lo0 = 2u * jf + 3u * lf;
                 span = max(span, hi >= lo0 ? hi - lo0 + 1u : 1u);
+                if (spix != nullptr) spix[q] = make_uint2(lo0, hi);
             }
-            // (clamped to the table's row stride: every reader takes ctrl[7] as
-            // is, and a position past it reads as "left the window")
+            // (rounded up to whole chunks of the pass's job queue (pix_chunk,
+            // spix: rows of one pixel per chunk) and clamped to the table's row
+            // stride, a multiple of it: every reader takes ctrl[7] as is, and a
+            // position past it reads as "left the window")
+            if (spix != nullptr && pix_chunk > 1u) span = (span + pix_chunk - 1u) / pix_chunk * pix_chunk;
             span = min(span, pix_emax);
             if (span) atomicMax(ctrl + 7, span);
         }
@@ -2909,12 +2945,12 @@ hipError_t launch_serial_tables(double *tab, double *scratch, uint32_t npix, uin
 hipError_t launch_serial_window(uint32_t *ctrl, const uint32_t *jump, uint32_t *win, uint32_t n,
                                 SerialPred M, uint32_t *lo, uint32_t L, uint32_t K, uint32_t depth,
                                 uint32_t nserial, uint32_t pix_spp, uint32_t pix_emax, uint32_t *counters,
-                                uint32_t ncounters, hipStream_t stream) {
+                                uint32_t ncounters, uint2 *spix, uint32_t pix_chunk, hipStream_t stream) {
     if (!n) return hipSuccess;
     const uint32_t threads = std::max((n + kWinPerThread - 1) / kWinPerThread, lo ? std::min(L, 1u << 16) : 0u);
     hipLaunchKernelGGL(serial_window_kernel, dim3((threads + 255) / 256), dim3(256), 0, stream, ctrl,
                        jump, win, n, M, lo, L, K, depth, nserial, pix_spp, pix_emax, counters,
-                       counters ? ncounters : 0u);
+                       counters ? ncounters : 0u, pix_spp != 0u ? spix : nullptr, pix_chunk);
     return hipGetLastError();
 }
 

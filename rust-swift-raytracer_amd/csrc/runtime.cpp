@@ -54,7 +54,7 @@ DeviceState::~DeviceState() {
                     sph_shade, sph_kind, tbvh_nodes, tbvh_tris, tbvh_loose, tw_nodes,
                     cam_nodes, cam_tris, ptl_off, ptl_items, spl, tile, gath,
                     sstates, stab, sscan, swin, sjump, sctrl, sbend, spath, sfin,
-                    gspl, gspl_rects, gspl_flag, scheck, slo, ssbend, ssb, sptab};
+                    gspl, gspl_rects, gspl_flag, scheck, slo, ssbend, ssb, sptab, sspix};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
     for (hipEvent_t e : ev)
@@ -670,6 +670,7 @@ int render_frame(WorldState &w, const CameraModel &cam, size_t width, size_t hei
         p.win = sp->win;
         p.sM = sp->M;
         p.slo = sp->lo;
+        p.spix = sp->spix;
         p.ctrl = sp->ctrl;
         p.max_draws = 2u + 3u * (uint32_t)std::max(o.max_ray_bounces, 0);
         p.njobs = (uint32_t)njobs;
@@ -1097,6 +1098,9 @@ static int serial_find_states(WorldState &w, const CameraModel &cam, size_t widt
         // instead of the count pass's L K, and independent ones, unlike the
         // coalescing search's chains.  RT_AMD_SERIAL_PIXTAB=0: the searches below.
         bool pixtab = spp >= 4 && env_u64("RT_AMD_SERIAL_PIXTAB", 1) != 0;
+        // the pixel pass's per-pixel spans (one load per refill, whole-chunk rows)
+        const bool use_spix = env_u64("RT_AMD_SERIAL_SPIX", 1) != 0;
+        const uint64_t pchunk = std::max<uint64_t>(1, env_u64("RT_AMD_SERIAL_PCHUNK", 128));
         bool coalesce = false;
         // (iterations of 128 k samples in blocks of 32 for the coalescing search,
         // profiles/round3_serial/coalesce_sweep*.log; 16 k for the count pass;
@@ -1193,6 +1197,8 @@ static int serial_find_states(WorldState &w, const CameraModel &cam, size_t widt
             // iteration touches x the widest span of positions one pixel's windows cover
             npq_max = L / spp + 2;
             emax = pixtab ? serial_pixtab_emax64(spp, K, depth) : 0;
+            // (rows padded to whole job chunks of the pixel pass: render_frame's chunk)
+            if (pixtab && use_spix) emax = (emax + pchunk - 1) / pchunk * pchunk;
             if (!pixtab || (npq_max * emax <= (1ull << 28) && emax <= 0x7FFFFFFFull)) break;
             // too large: plan the iterations as without the pixel table (L, and
             // with it K and the reach; the coalescing search where the rule picks it)
@@ -1206,6 +1212,7 @@ static int serial_find_states(WorldState &w, const CameraModel &cam, size_t widt
         const bool pgather = pixtab && env_u64("RT_AMD_SERIAL_PGATHER", 0) != 0;
         if (pixtab) {
             HIP_TRY(grow(d->sptab, d->sptab_cap, npq_max * emax));
+            HIP_TRY(grow(d->sspix, d->sspix_cap, npq_max));
             if (pgather) HIP_TRY(grow(d->samples, d->samples_cap, L * K));
         }
         // The walks size each iteration's windows from the per-pixel variances
@@ -1296,11 +1303,14 @@ static int serial_find_states(WorldState &w, const CameraModel &cam, size_t widt
                 HIP_TRY(launch_serial_window(d->sctrl, d->sjump, d->swin, (uint32_t)wlen, pred, d->slo,
                                              (uint32_t)L, (uint32_t)K, depth, (uint32_t)N,
                                              pixtab ? (uint32_t)spp : 0u, (uint32_t)emax,
-                                             pixtab ? d->counter : nullptr, kPixtabParts, s));
+                                             pixtab ? d->counter : nullptr, kPixtabParts,
+                                             pixtab && use_spix ? d->sspix : nullptr,
+                                             (uint32_t)pchunk, s));
                 if (pixtab) {
                     SerialPass sp{kRngSerialPixel, 0u, (uint32_t)npq_max, (uint32_t)emax, d->swin, pred, d->sctrl,
                                   d->slo};
                     sp.ptab = d->sptab;
+                    sp.spix = use_spix ? d->sspix : nullptr;
                     sp.L = (uint32_t)L;
                     sp.Kmax = (uint32_t)K;
                     rc = render_frame(w, cam, width, height, ob, nullptr, s, nullptr, &sp);
@@ -1353,6 +1363,28 @@ static int serial_find_states(WorldState &w, const CameraModel &cam, size_t widt
                 std::fprintf(stderr, "serial debug: coalesce %llu traces in %llu blocks (%.3f of the count pass's "
                              "%llu), %.1f trace passes per block\n", c[0], c[2], (double)c[0] / std::max(1.0, (double)c[3]),
                              c[3], (double)c[1] / (double)c[2]);
+        }
+        if (env_u64("RT_AMD_SERIAL_DEBUG", 0) && pixtab) {
+            // the pixel table pass's idle jobs: per iteration every pixel's row is E
+            // (the widest span) long, a pixel's own span ~ 2 (spp - 1) + 3 (K - 1) +
+            // 3 (spp - 1) mu (its predicted scatters)
+            std::vector<double> mu(npix);
+            HIP_TRY(hipMemcpy(mu.data(), d->stab + npix + 1, npix * sizeof(double), hipMemcpyDeviceToHost));
+            const uint64_t npq = std::max<uint64_t>(1, L / spp);
+            double used = 0, padded = 0;
+            for (uint64_t q0 = 0; q0 < npix; q0 += npq) {
+                double mx = 0, sum = 0;
+                const uint64_t q1 = std::min(npix, q0 + npq);
+                for (uint64_t q = q0; q < q1; ++q) {
+                    const double sp = 2.0 * (spp - 1) + 3.0 * (K - 1) + 3.0 * (spp - 1) * mu[q] + 1;
+                    mx = std::max(mx, sp);
+                    sum += sp;
+                }
+                used += sum;
+                padded += mx * (double)(q1 - q0);
+            }
+            std::fprintf(stderr, "serial debug: pixel table spans use %.3f of the npq x E jobs (K %llu)\n",
+                         used / std::max(padded, 1.0), (unsigned long long)K);
         }
         if (env_u64("RT_AMD_SERIAL_DEBUG", 0)) {
             std::fprintf(stderr, "serial debug: %s N %llu L %llu R %llu K %llu sigma %.3f: %u iterations (%u "

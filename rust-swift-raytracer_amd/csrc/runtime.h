@@ -91,6 +91,7 @@ struct DeviceState {
     uint32_t *sbend = nullptr;       size_t sbend_cap = 0;
     uint32_t *spath = nullptr;       size_t spath_cap = 0;  // block walks' paths (L x K)
     float *sptab = nullptr;          size_t sptab_cap = 0;  // pixel table pass: b per (pixel, position)
+    uint2 *sspix = nullptr;          size_t sspix_cap = 0;  // pixel table pass: {plo, phi} per pixel
     uint32_t *sfin = nullptr;                               // chain result (4 + kMaxWalkBlocks)
     uint32_t *sjump = nullptr;
     uint32_t *sctrl = nullptr;
@@ -173,6 +174,7 @@ struct SerialPass {
     // positions, the launch's bounds), the iteration length and its K
     float *ptab = nullptr;
     uint32_t L = 0, Kmax = 0;
+    const uint2 *spix = nullptr;  // its pixels' position spans (serial_window_kernel)
 };
 
 // Renders rank's tile of a width x height frame into device memory d_out
