@@ -396,10 +396,12 @@ static uint32_t node_word(const float *lo_a, const float *hi_b) {  // a, b bits 
 // (tools/tbvh_sim.cpp SIM_FIXED_OCT) but cost a second cache line per step.
 static void quantize_boxes(const std::vector<float> &nodes, size_t stride, bool normals,
                            const std::vector<uint32_t> &miss, std::vector<uint32_t> &q, QuantGrid &g,
-                           float *nbase, float *nstep) {
+                           float *nbase, float *nstep, const float *glo = nullptr, const float *ghi = nullptr) {
     const size_t n = nodes.size() / stride;
     float lo[3], hi[3], nlo = 1, nhi = -1;
     for (int k = 0; k < 3; ++k) { lo[k] = nodes[k]; hi[k] = nodes[4 + k]; }  // root holds all
+    if (glo)  // a grid over a given box holding the root's (per-cell trees: one grid for all)
+        for (int k = 0; k < 3; ++k) { lo[k] = std::min(lo[k], glo[k]); hi[k] = std::max(hi[k], ghi[k]); }
     for (size_t i = 0; i < n && normals; ++i)
         for (int k = 0; k < 3; ++k) {
             nlo = std::min(nlo, nodes[i * stride + 8 + k]);
@@ -613,6 +615,76 @@ void build_wide_image(TriangleBVH &tb) {
         }
         tb.wdepth = std::max(tb.wdepth, depth[w]);
     }
+}
+
+TriangleCells build_triangle_cells(const std::vector<Triangle> &tris, const std::vector<float> &tri_hot,
+                                   uint32_t leaf_size, float size, TriangleBVH &tb) {
+    TriangleCells out;
+    if (tb.nodes.empty() || tb.wnodes.empty() || !(size > 0)) return out;
+    // cells over the box of the mesh's (finite) vertices
+    double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+    for (const Triangle &t : tris)
+        for (const Vec3 &v : {t.v0, t.v1, t.v2}) {
+            const double c[3] = {v.x, v.y, v.z};
+            if (!(std::isfinite(c[0]) && std::isfinite(c[1]) && std::isfinite(c[2]))) continue;
+            for (int k = 0; k < 3; ++k) { lo[k] = std::min(lo[k], c[k]); hi[k] = std::max(hi[k], c[k]); }
+        }
+    uint64_t ncells = 1;
+    for (int k = 0; k < 3; ++k) {
+        if (!(lo[k] <= hi[k])) return out;
+        out.lo[k] = (float)lo[k];
+        out.n[k] = (uint32_t)std::max(1.0, std::ceil((hi[k] - out.lo[k]) / size + 1e-9));
+        ncells *= out.n[k];
+    }
+    if (ncells > 4096) return out;
+    out.size = size;
+    out.ncells = (uint32_t)ncells;
+    // one tree per cell, on host threads (SAH scale: the cell's half-diagonal,
+    // as the emulation, tools/tbvh_sim.cpp SIM_CELL)
+    std::vector<TriangleBVH> trees(ncells);
+    std::atomic<uint64_t> next{0};
+    auto work = [&]() {
+        for (uint64_t c; (c = next++) < ncells;) {
+            const uint64_t x = c % out.n[0], y = (c / out.n[0]) % out.n[1], z = c / (out.n[0] * out.n[1]);
+            const float oc[3] = {out.lo[0] + ((float)x + 0.5f) * size, out.lo[1] + ((float)y + 0.5f) * size,
+                                 out.lo[2] + ((float)z + 0.5f) * size};
+            trees[c] = build_triangle_bvh(tris, tri_hot, leaf_size, oc, size * 0.866);
+        }
+    };
+    const unsigned nt = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    std::vector<std::thread> pool;
+    for (unsigned i = 1; i < nt; ++i) pool.emplace_back(work);
+    work();
+    for (auto &t : pool) t.join();
+    // one grid for every tree (and the static one): the union of their roots
+    float glo[3], ghi[3];
+    for (int k = 0; k < 3; ++k) { glo[k] = tb.nodes[k]; ghi[k] = tb.nodes[4 + k]; }
+    for (const TriangleBVH &t : trees) {
+        if (t.nodes.empty() || t.wnodes.empty()) return TriangleCells{};
+        for (int k = 0; k < 3; ++k) { glo[k] = std::min(glo[k], t.nodes[k]); ghi[k] = std::max(ghi[k], t.nodes[4 + k]); }
+    }
+    trees.push_back(tb);
+    uint64_t sw = 0, sr = 0;
+    for (TriangleBVH &t : trees) {
+        quantize_boxes(t.nodes, 16, true, t.miss, t.qnodes, t.qbox, &t.nbase, &t.nstep, glo, ghi);
+        build_wide_image(t);
+        if (t.wnodes.empty()) return TriangleCells{};
+        sw = std::max<uint64_t>(sw, t.wnodes.size() / 32);
+        sr = std::max<uint64_t>(sr, t.tris.size() / 16);
+        out.wdepth = std::max(out.wdepth, t.wdepth);
+        out.mag = std::max(out.mag, t.mag);
+    }
+    if ((ncells + 1) * sw >= (1ull << 32) || (ncells + 1) * sr * 4 >= (1ull << 32)) return TriangleCells{};
+    out.stride_w = (uint32_t)sw;
+    out.stride_r = (uint32_t)sr;
+    out.wnodes.assign((ncells + 1) * sw * 32, 0u);
+    out.tris.assign((ncells + 1) * sr * 16, 0.0f);
+    for (uint64_t c = 0; c <= ncells; ++c) {
+        std::copy(trees[c].wnodes.begin(), trees[c].wnodes.end(), out.wnodes.begin() + c * sw * 32);
+        std::copy(trees[c].tris.begin(), trees[c].tris.end(), out.tris.begin() + c * sr * 16);
+    }
+    tb = trees.back();  // (the static tree on the common grid: its binary walk's nodes too)
+    return out;
 }
 
 CameraTriangleBVH build_camera_triangle_bvh(const std::vector<Triangle> &tris,

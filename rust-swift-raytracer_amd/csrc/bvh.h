@@ -91,6 +91,32 @@ struct TriangleBVH {
 // Fills tb.wnodes / tb.wdepth from tb.qnodes (build_triangle_bvh calls it).
 void build_wide_image(TriangleBVH &tb);
 
+// Per-origin-cell triangle trees (RT_AMD_TRI_CELLS): the box of
+// the mesh cut into n[0] x n[1] x n[2] cubic cells of edge `size` from `lo`;
+// tree c (c = (z n1 + y) n0 + x) holds the phantoms of origin = its cell's
+// centre (build_triangle_bvh with oc), so a secondary ray whose origin lies in
+// the cell is widened by at most the cell's half-diagonal; tree ncells is the
+// static tree (rays from outside every cell).  Every tree is exact for any
+// origin (the per-ray widening covers o - oc), so the choice of tree only
+// changes the work.  All trees share one quantisation grid (the union of their
+// root boxes; the static tree tb is re-quantised on it), so the kernel's grid
+// parameters stay per launch.  Wide images and records are concatenated with
+// fixed strides (wide nodes, records).
+struct TriangleCells {
+    float lo[3] = {0, 0, 0};
+    float size = 0;
+    uint32_t n[3] = {0, 0, 0};
+    uint32_t ncells = 0;
+    std::vector<uint32_t> wnodes;   // (ncells + 1) x stride_w wide nodes of 32 u32
+    std::vector<float> tris;        // (ncells + 1) x stride_r records of 16 floats
+    uint32_t stride_w = 0, stride_r = 0, wdepth = 0;
+    float mag = 0;                  // largest |coordinate| over the trees (rho)
+};
+// Empty (ncells == 0) when a tree has no wide image or the trees do not fit
+// the kernel's 32-bit indices.
+TriangleCells build_triangle_cells(const std::vector<Triangle> &tris, const std::vector<float> &tri_hot,
+                                   uint32_t leaf_size, float size, TriangleBVH &tb);
+
 // tri_hot: PackedScene::tri_hot (the exact per-triangle n and n.v0 bits).
 // oc (optional): origin the boxes are built for; phantom: SAH weight of the
 // normal spread (<= 0: derived from the scene).

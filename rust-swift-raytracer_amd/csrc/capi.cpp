@@ -77,6 +77,20 @@ Rust_WorldHandle *load_world(const char *source) {
     world->state.tbvh = rtamd::build_triangle_bvh(world->state.scene.triangles,
                                                   world->state.packed.tri_hot,
                                                   env_leaf("RT_AMD_TRI_LEAF", 1u));
+    // per-origin-cell trees, RT_AMD_TRI_CELLS=<cell edge> (measured and left
+    // off): the static tree is re-quantised on their common grid
+    if (const char *cs = std::getenv("RT_AMD_TRI_CELLS")) {
+        const float size = std::strtof(cs, nullptr);
+        if (size > 0.0f)
+            world->state.tcells = rtamd::build_triangle_cells(world->state.scene.triangles,
+                                                              world->state.packed.tri_hot,
+                                                              env_leaf("RT_AMD_TRI_LEAF", 1u), size,
+                                                              world->state.tbvh);
+        const auto &tc = world->state.tcells;
+        std::fprintf(stderr, "tri cells: %u x %u x %u = %u cells of %.3g, %u wide nodes and %u records per tree, "
+                     "%.1f MB\n", tc.n[0], tc.n[1], tc.n[2], tc.ncells, tc.size, tc.stride_w, tc.stride_r,
+                     (tc.wnodes.size() * 4.0 + tc.tris.size() * 4.0) / 1e6);
+    }
     // bounce-0 triangle tree for the scene camera (rebuilt by the first render
     // after move_camera_position, which does not see the world)
     rtamd::prepare_camera(world->state, world->state.scene.camera);

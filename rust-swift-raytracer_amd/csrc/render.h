@@ -137,6 +137,13 @@ struct TraceParams {
     const uint4 *tw_nodes;    // 8 per wide node (128 B)
     uint32_t tw_depth;        // stack entries per lane (3 * TriangleBVH::wdepth, >= 1)
     uint32_t wsteps;          // wide-node fetches per lane per loop iteration (sliced walks)
+    // per-origin-cell trees (bvh.h TriangleCells; tc_ncells == 0: the static
+    // tree only): tree c's wide nodes from tw_nodes + 8 c tw_stride, its records
+    // from tw_tris + 4 c tw_rstride; tree tc_ncells is the static tree
+    const float4 *tw_tris;
+    uint32_t tw_stride, tw_rstride, tc_ncells;
+    uint32_t tc_n[3];
+    float tc_lo[3], tc_size, tc_inv_size;
     float cq_base[3], cq_step[3];                      // camera-tree grid
     // the same triangles' phantoms for the camera origin (bvh.h CameraTriangleBVH),
     // used at bounce 0; cam_nnodes == 0: bounce 0 uses the tree above
@@ -168,8 +175,10 @@ struct TraceParams {
     FastDiv div_sspp;         // ... and its divider
     uint32_t max_draws;       // 2 + 3 * max(depth, 0): bound of the draw count search
     uint32_t sL, sK;          // kRngSerialPixel: the iteration length and the launch's K
-    const uint2 *spix;        // kRngSerialPixel (optional): per local pixel its positions
-                              // {plo, phi} (serial_window_kernel), one load per refill
+    const uint4 *spix;        // kRngSerialPixel (optional): per local pixel its positions
+                              // {plo, phi} and the positions [z, w] (relative to plo; empty
+                              // when z > w) copied from the previous iteration's table
+                              // (serial_window_kernel, serial_reuse_kernel): not traced
     // frames of one rank whose global job indices (row * W + col) * spp + s
     // fit 32 bits (gj32 != 0): the global job of launch job j in local row q is
     // j + gj_c0 - q * gj_2p (mod 2^32), gj_c0 = (H - 1 - slab_row0) W spp,
@@ -246,7 +255,15 @@ constexpr uint32_t kSerialJumpWords = 32 * (64 + kSerialJumpT1 + 256);
 hipError_t launch_serial_window(uint32_t *ctrl, const uint32_t *jump, uint32_t *win, uint32_t n,
                                 SerialPred M, uint32_t *lo, uint32_t L, uint32_t K, uint32_t depth,
                                 uint32_t nserial, uint32_t pix_spp, uint32_t pix_emax, uint32_t *counters,
-                                uint32_t ncounters, uint2 *spix, uint32_t pix_chunk, hipStream_t stream);
+                                uint32_t ncounters, uint4 *spix, uint32_t pix_chunk, const uint4 *spix_prev,
+                                hipStream_t stream);
+// The pixel table's entries the previous iteration already traced (window
+// kernel: spix[q].zw, relative to the pixel's plo) copied from ptab_prev
+// (row stride ctrl[11], its pixels from frame pixel ctrl[10] / spp, stream
+// offset ctrl[8] between the two iterations' windows) into ptab (ctrl[7]).
+hipError_t launch_serial_reuse(const uint32_t *ctrl, const uint4 *spix, const uint4 *spix_prev, float *ptab,
+                               const float *ptab_prev, uint32_t npq_max, uint32_t spp, uint32_t L,
+                               uint32_t nserial, hipStream_t stream);
 // The pixel table pass's result (ptab: b of local pixel q at position plo(q) + e
 // = ptab[q * ctrl[7] + e]) gathered into the count table of the iteration
 // (table[jl * K + k], the layout the walks read; -1 outside the traced span)

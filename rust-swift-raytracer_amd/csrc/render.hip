@@ -142,11 +142,11 @@ __device__ __forceinline__ uint32_t uniform_load_u32(const uint32_t *base, uint3
 #endif
 }
 
-__device__ __forceinline__ uint2 uniform_load_u2(const uint2 *base, uint32_t i) {
+__device__ __forceinline__ uint4 uniform_load_u4(const uint4 *base, uint32_t i) {
 #if defined(__HIP_DEVICE_COMPILE__)
     typedef const __attribute__((address_space(4))) uint32_t *cu32_ptr;
-    const cu32_ptr q = (cu32_ptr)(const void *)base + 2u * i;
-    return make_uint2(q[0], q[1]);
+    const cu32_ptr q = (cu32_ptr)(const void *)base + 4u * i;
+    return make_uint4(q[0], q[1], q[2], q[3]);
 #else
     return base[i];
 #endif
@@ -644,8 +644,9 @@ __device__ __forceinline__ bool tri_wide_child(const TraceParams &p, uint32_t w0
 
 __device__ __forceinline__ void tri_leaf(const TraceParams &p, F3 org, F3 dir, bool cam,
                                          uint32_t leaf, float best_t, float &tri_t, int &tri_i,
-                                         uint32_t &tri_in, uint32_t &tri_done) {
-    const float4 *recs = cam ? p.cam_tris : p.tbvh_tris;
+                                         uint32_t &tri_in, uint32_t &tri_done, const float4 *wrecs = nullptr) {
+    // (wrecs: the per-cell tree's records, kMesh 3 with TraceParams::tc_ncells)
+    const float4 *recs = wrecs ? wrecs : cam ? p.cam_tris : p.tbvh_tris;
     const uint32_t first = leaf >> 3, end = first + (leaf & 7u);
     tri_done += leaf & 7u;
     for (uint32_t j = first; j < end; ++j)
@@ -693,7 +694,7 @@ __device__ __forceinline__ void job_pixel(const TraceParams &p, uint32_t job, ui
 __device__ __forceinline__ void serial_pixel_span(const TraceParams &p, uint32_t q, uint32_t &plo,
                                                   uint32_t &phi) {
     if (p.spix != nullptr) {  // tabulated by the window kernel: one load
-        const uint2 s = p.spix[q];
+        const uint4 s = p.spix[q];
         plo = s.x;
         phi = s.y;
         return;
@@ -1061,6 +1062,9 @@ void trace_kernel(TraceParams p) {
 #endif
 
     uint32_t pool_next = 0, pool_end = 0;  // wave-uniform job pool
+    // (kSerial pixel pass) jobs [gap_lo, gap_lo + gap_len) of the pool are not
+    // handed out: the pool counts jobs without them (copied table entries)
+    uint32_t gap_lo = ~0u, gap_len = 0;
     bool exhausted = false;
 
     // Where a finished sample goes: the slab (slot = job) or, with the fused
@@ -1302,8 +1306,31 @@ void trace_kernel(TraceParams p) {
                 // (tri_merge keeps the (t, index) argmin).
                 const TraceParams &p = kargs();  // (see kargs)
                 uint32_t wbudget = p.wsteps;
-                const F3 dlt2 = f3(2.0f * (org.x - p.tbvh_oc[0]), 2.0f * (org.y - p.tbvh_oc[1]),
-                                   2.0f * (org.z - p.tbvh_oc[2]));
+                // Per-origin-cell trees (RT_AMD_TRI_CELLS, off by default): the
+                // tree whose phantoms were built for the centre of the cell the
+                // origin lies in (the static tree, tc_ncells, outside every cell).
+                // The origin does not change during the walk, so every slice
+                // picks the same tree.  Any tree is exact for any origin: the
+                // widening below covers o - oc (bvh.h TriangleCells).
+                F3 oc = f3(p.tbvh_oc[0], p.tbvh_oc[1], p.tbvh_oc[2]);
+                uint32_t wbase = 0;
+                const float4 *wrecs = nullptr;
+                if (p.tc_ncells != 0u) {
+                    const float fx = floorf((org.x - p.tc_lo[0]) * p.tc_inv_size);
+                    const float fy = floorf((org.y - p.tc_lo[1]) * p.tc_inv_size);
+                    const float fz = floorf((org.z - p.tc_lo[2]) * p.tc_inv_size);
+                    uint32_t tree = p.tc_ncells;
+                    if (fx >= 0.0f && fx < (float)p.tc_n[0] && fy >= 0.0f && fy < (float)p.tc_n[1] && fz >= 0.0f &&
+                        fz < (float)p.tc_n[2]) {
+                        tree = ((uint32_t)fz * p.tc_n[1] + (uint32_t)fy) * p.tc_n[0] + (uint32_t)fx;
+                        // (bvh.cpp build_triangle_cells' centre, the same operations)
+                        oc = f3(p.tc_lo[0] + (fx + 0.5f) * p.tc_size, p.tc_lo[1] + (fy + 0.5f) * p.tc_size,
+                                p.tc_lo[2] + (fz + 0.5f) * p.tc_size);
+                    }
+                    wbase = tree * p.tw_stride;
+                    wrecs = p.tw_tris + (size_t)4u * tree * p.tw_rstride;
+                }
+                const F3 dlt2 = f3(2.0f * (org.x - oc.x), 2.0f * (org.y - oc.y), 2.0f * (org.z - oc.z));
                 F3 nlo, nhi;
                 sphere_slabs(org, inv, e, nlo, nhi);
                 // (the grid base folded in: tri_wide_child)
@@ -1313,7 +1340,7 @@ void trace_kernel(TraceParams p) {
                          __builtin_fmaf(p.tq_base[2], inv.z, nhi.z));
                 float cap = fminf(best_t, tri_t);
                 do {
-                    const uint4 *wn = p.tw_nodes + 8u * node;
+                    const uint4 *wn = p.tw_nodes + 8u * (wbase + node);
                     tnode_tests += 4;
                     float tn[4];
                     bool in[4];
@@ -1351,7 +1378,8 @@ void trace_kernel(TraceParams p) {
                         const uint32_t c = (uint32_t)__builtin_ctz(lmask);
                         lmask &= lmask - 1u;
                         const uint32_t lw = c == 0 ? a[0] : c == 1 ? a[1] : c == 2 ? a[2] : a[3];
-                        tri_leaf(p, org, dir, false, lw & ~kLeafBitDev, best_t, tri_t, tri_i, tri_in, tri_done);
+                        tri_leaf(p, org, dir, false, lw & ~kLeafBitDev, best_t, tri_t, tri_i, tri_in, tri_done,
+                                 wrecs);
                     }
                     cap = fminf(best_t, tri_t);
                     uint32_t nxt = 0xFFFFu;
@@ -1579,9 +1607,23 @@ void trace_kernel(TraceParams p) {
                         // positions inside the pixel's span (the rest would leave
                         // lanes idle, serial_pixel_job) and skip chunks past it
                         const uint32_t q = fdiv(base, pc.div_spp);
-                        const uint2 sq = uniform_load_u2(pc.spix, q);
-                        const uint32_t live_end = q * pc.spp + (sq.y >= sq.x ? sq.y - sq.x + 1u : 0u);
+                        const uint4 sq = uniform_load_u4(pc.spix, q);
+                        const uint32_t rowb = q * pc.spp;
+                        const uint32_t live_end = rowb + (sq.y >= sq.x ? sq.y - sq.x + 1u : 0u);
                         pool_end = min(pool_end, live_end);
+                        // the positions the previous iteration traced were copied
+                        // (serial_reuse_kernel): the pool skips them
+                        gap_lo = ~0u;
+                        gap_len = 0;
+                        if (sq.z <= sq.w && pool_next < pool_end) {
+                            const uint32_t g0 = max(rowb + sq.z, pool_next);
+                            const uint32_t g1 = min(rowb + sq.w + 1u, pool_end);
+                            if (g0 < g1) {
+                                gap_lo = g0;
+                                gap_len = g1 - g0;
+                                pool_end -= gap_len;
+                            }
+                        }
                         if (pool_next >= pool_end) continue;
                     }
 #ifdef RT_WAVE_TIMES
@@ -1602,7 +1644,8 @@ void trace_kernel(TraceParams p) {
             const uint32_t rank = __builtin_amdgcn_mbcnt_hi(
                 (uint32_t)(dead >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)dead, 0u));
             if (!active && rank < avail) {
-                const uint32_t job = pool_next + rank;
+                uint32_t job = pool_next + rank;
+                if (kSerial && job >= gap_lo) job += gap_len;
                 // Jobs are enumerated pixel-major (job = pixel*spp + s): the
                 // lanes refilled together trace samples of one pixel (or of
                 // neighbours), so their primary walks visit the same nodes
@@ -1936,7 +1979,8 @@ __global__ __launch_bounds__(256) void serial_window_kernel(uint32_t *__restrict
                                                             uint32_t L, uint32_t Kmax, uint32_t depth,
                                                             uint32_t nserial, uint32_t pix_spp, uint32_t pix_emax,
                                                             uint32_t *__restrict__ counters, uint32_t ncounters,
-                                                            uint2 *__restrict__ spix, uint32_t pix_chunk) {
+                                                            uint4 *__restrict__ spix, uint32_t pix_chunk,
+                                                            const uint4 *__restrict__ spix_prev) {
     if (ctrl[0] != 0u) return;
     // the following trace pass's job counters (instead of a fill launch)
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < ncounters; i += gridDim.x * blockDim.x)
@@ -1952,6 +1996,13 @@ __global__ __launch_bounds__(256) void serial_window_kernel(uint32_t *__restrict
             // 2 jf + 3 lo(jf) to 2 jz + 3 (lo(jz) + K - 1)
             const uint32_t ln = min(L, nserial - a);
             const uint32_t p0 = a / pix_spp, npq = (a + ln - 1u) / pix_spp - p0 + 1u;
+            // the previous iteration (serial_walk_finish_kernel: its first sample
+            // ctrl[10], its table's row stride ctrl[11], this iteration's window
+            // at its stream offset ctrl[8]; ctrl[9] set once one has run)
+            const bool reuse = spix_prev != nullptr && ctrl[9] != 0u && ctrl[11] != 0u;
+            const uint32_t ap = ctrl[10], D = ctrl[8], Ep = ctrl[11];
+            const uint32_t p0p = ap / pix_spp;
+            const uint32_t npqp = reuse ? (ap + min(L, nserial - ap) - 1u) / pix_spp - p0p + 1u : 0u;
             uint32_t span = 0;
             for (uint32_t q = blockIdx.x * blockDim.x + threadIdx.x; q < npq; q += gridDim.x * blockDim.x) {
                 const uint32_t jf = q == 0u ? 0u : (p0 + q) * pix_spp - a;
@@ -1960,7 +2011,27 @@ __global__ __launch_bounds__(256) void serial_window_kernel(uint32_t *__restrict
                 const uint32_t lz = serial_lo(M, a, jz, K, depth, nserial);
                 const uint32_t hi = 2u * jz + 3u * (lz + K - 1u), lo0 = 2u * jf + 3u * lf;
                 span = max(span, hi >= lo0 ? hi - lo0 + 1u : 1u);
-                if (spix != nullptr) spix[q] = make_uint2(lo0, hi);
+                if (spix != nullptr) {
+                    // the positions of this pixel the previous table holds: its
+                    // traced range [plo', min(phi', plo' + E' - 1)] at offset -D,
+                    // inside [lo0, hi] (relative to lo0; empty: z > w)
+                    uint32_t r0 = 1u, r1 = 0u;
+                    const uint32_t pix = p0 + q;
+                    if (reuse && pix >= p0p && pix - p0p < npqp) {
+                        const uint4 so = spix_prev[pix - p0p];
+                        if (so.y >= so.x) {
+                            const int64_t olo = (int64_t)so.x - D;
+                            const int64_t ohi = (int64_t)min(so.y, so.x + Ep - 1u) - D;
+                            const int64_t l = olo > (int64_t)lo0 ? olo : (int64_t)lo0;
+                            const int64_t h = ohi < (int64_t)hi ? ohi : (int64_t)hi;
+                            if (l <= h) {
+                                r0 = (uint32_t)(l - lo0);
+                                r1 = (uint32_t)(h - lo0);
+                            }
+                        }
+                    }
+                    spix[q] = make_uint4(lo0, hi, r0, r1);
+                }
             }
             // (rounded up to whole chunks of the pass's job queue (pix_chunk,
             // spix: rows of one pixel per chunk) and clamped to the table's row
@@ -2367,6 +2438,13 @@ __global__ __launch_bounds__(256) void serial_walk_finish_kernel(
         ctrl[2] += B;
         ctrl[3] += 1u;
         ctrl[4] = a + done;
+        // (the next iteration's reuse of this one's pixel table: its window
+        // starts at offset D = 2 done + 3 B of this one's; the first sample and
+        // the row stride of this one's table)
+        ctrl[8] = 2u * done + 3u * B;
+        ctrl[9] = 1u;
+        ctrl[10] = a;
+        ctrl[11] = ctrl[7];
         ctrl[7] = 0u;  // (the next window kernel's pixel span, atomicMax)
         if (a + done >= nserial) ctrl[0] = 1u;
         if (V != nullptr) {
@@ -2945,12 +3023,50 @@ hipError_t launch_serial_tables(double *tab, double *scratch, uint32_t npix, uin
 hipError_t launch_serial_window(uint32_t *ctrl, const uint32_t *jump, uint32_t *win, uint32_t n,
                                 SerialPred M, uint32_t *lo, uint32_t L, uint32_t K, uint32_t depth,
                                 uint32_t nserial, uint32_t pix_spp, uint32_t pix_emax, uint32_t *counters,
-                                uint32_t ncounters, uint2 *spix, uint32_t pix_chunk, hipStream_t stream) {
+                                uint32_t ncounters, uint4 *spix, uint32_t pix_chunk, const uint4 *spix_prev,
+                                hipStream_t stream) {
     if (!n) return hipSuccess;
     const uint32_t threads = std::max((n + kWinPerThread - 1) / kWinPerThread, lo ? std::min(L, 1u << 16) : 0u);
     hipLaunchKernelGGL(serial_window_kernel, dim3((threads + 255) / 256), dim3(256), 0, stream, ctrl,
                        jump, win, n, M, lo, L, K, depth, nserial, pix_spp, pix_emax, counters,
-                       counters ? ncounters : 0u, pix_spp != 0u ? spix : nullptr, pix_chunk);
+                       counters ? ncounters : 0u, pix_spp != 0u ? spix : nullptr, pix_chunk,
+                       pix_spp != 0u && spix != nullptr ? spix_prev : nullptr);
+    return hipGetLastError();
+}
+
+// One workgroup per local pixel q of the iteration: the table entries of its
+// reused range (spix[q].zw, serial_window_kernel) from the previous table.
+// Entry e of pixel q is stream position plo(q) + e of this iteration's window,
+// i.e. position plo(q) + e + D of the previous one, entry plo(q) + e + D -
+// plo'(q') of its pixel's row there: b of a (pixel, stream position) pair is
+// the same whichever iteration traced it.
+__global__ __launch_bounds__(256) void serial_reuse_kernel(const uint32_t *__restrict__ ctrl,
+                                                           const uint4 *__restrict__ spix,
+                                                           const uint4 *__restrict__ spix_prev,
+                                                           float *__restrict__ ptab,
+                                                           const float *__restrict__ ptab_prev, uint32_t spp,
+                                                           uint32_t L, uint32_t nserial) {
+    if (ctrl[0] != 0u || ctrl[9] == 0u) return;
+    const uint32_t a = ctrl[4];
+    const uint32_t ln = min(L, nserial - a);
+    const uint32_t p0 = a / spp, npq = (a + ln - 1u) / spp - p0 + 1u;
+    const uint32_t q = blockIdx.x;
+    if (q >= npq) return;
+    const uint4 s = spix[q];
+    if (s.z > s.w) return;
+    const uint32_t E = ctrl[7], Ep = ctrl[11], D = ctrl[8];
+    const uint4 so = spix_prev[p0 + q - ctrl[10] / spp];
+    const uint32_t e1 = min(s.w, E - 1u);
+    for (uint32_t e = s.z + threadIdx.x; e <= e1; e += blockDim.x)
+        ptab[(size_t)q * E + e] = ptab_prev[(size_t)(p0 + q - ctrl[10] / spp) * Ep + (s.x + e + D - so.x)];
+}
+
+hipError_t launch_serial_reuse(const uint32_t *ctrl, const uint4 *spix, const uint4 *spix_prev, float *ptab,
+                               const float *ptab_prev, uint32_t npq_max, uint32_t spp, uint32_t L,
+                               uint32_t nserial, hipStream_t stream) {
+    if (!npq_max) return hipSuccess;
+    hipLaunchKernelGGL(serial_reuse_kernel, dim3(npq_max), dim3(256), 0, stream, ctrl, spix, spix_prev, ptab,
+                       ptab_prev, spp, L, nserial);
     return hipGetLastError();
 }
 

@@ -51,10 +51,10 @@ DeviceState::~DeviceState() {
     if (hipSetDevice(device) != hipSuccess) return;
     void *bufs[] = {sph_hot, sph_cold, tri_hot, tri_geo, mats, samples, ring, out, replay, counter, stats,
                     bvh_nodes, bvh_prims, big_hot, bvh_miss, bvh_prim_id, big_id, bvh_miss16,
-                    sph_shade, sph_kind, tbvh_nodes, tbvh_tris, tbvh_loose, tw_nodes,
+                    sph_shade, sph_kind, tbvh_nodes, tbvh_tris, tbvh_loose, tw_nodes, tw_tris,
                     cam_nodes, cam_tris, ptl_off, ptl_items, spl, tile, gath,
                     sstates, stab, sscan, swin, sjump, sctrl, sbend, spath, sfin,
-                    gspl, gspl_rects, gspl_flag, scheck, slo, ssbend, ssb, sptab, sspix};
+                    gspl, gspl_rects, gspl_flag, scheck, slo, ssbend, ssb, sptab, sspix, sptab2};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
     for (hipEvent_t e : ev)
@@ -117,7 +117,7 @@ static int device_for(WorldState &w, int want, DeviceState *&out) {
         // exists and every lane's stack fits in LDS beside a workgroup's tree
         // (RT_AMD_TRI_WIDE=0: the binary walk)
         const TriangleBVH &tw = w.tbvh;
-        const uint32_t tw_depth = std::max<uint32_t>(1u, 3u * tw.wdepth);
+        const uint32_t tw_depth = std::max<uint32_t>(1u, 3u * std::max(tw.wdepth, w.tcells.wdepth));
         bool wide = !tw.wnodes.empty() && env_u64("RT_AMD_TRI_WIDE", 1) != 0 &&
                     (size_t)tw_depth * trace_block_threads(true, 3, 0) * 2u <= 64u * 1024u;
         int tri = wide ? 3 : trace_mesh_kind(w.packed.ntri > 0, !w.tbvh.nodes.empty());
@@ -234,7 +234,12 @@ static int device_for(WorldState &w, int want, DeviceState *&out) {
             HIP_TRY(upu((void **)&d->tbvh_loose, tb.loose));
             d->tnodes = (uint32_t)(tb.qnodes.size() / 8);
             if (wide) {
-                HIP_TRY(upu((void **)&d->tw_nodes, tb.wnodes));
+                if (w.tcells.ncells) {  // the per-cell trees + the static one
+                    HIP_TRY(upu((void **)&d->tw_nodes, w.tcells.wnodes));
+                    HIP_TRY(up((void **)&d->tw_tris, w.tcells.tris));
+                } else {
+                    HIP_TRY(upu((void **)&d->tw_nodes, tb.wnodes));
+                }
                 d->tw_depth = tw_depth;
             }
             d->ttris = (uint32_t)(tb.tris.size() / 16);
@@ -593,11 +598,21 @@ int render_frame(WorldState &w, const CameraModel &cam, size_t width, size_t hei
         if (d->tw_nodes) {
             p.tw_nodes = d->tw_nodes;
             p.tw_depth = d->tw_depth;
+            if (d->tw_tris) {
+                const TriangleCells &tc = w.tcells;
+                p.tw_tris = (const float4 *)d->tw_tris;
+                p.tw_stride = tc.stride_w;
+                p.tw_rstride = tc.stride_r;
+                p.tc_ncells = tc.ncells;
+                for (int k = 0; k < 3; ++k) { p.tc_n[k] = tc.n[k]; p.tc_lo[k] = tc.lo[k]; }
+                p.tc_size = tc.size;
+                p.tc_inv_size = 1.0f / tc.size;
+            }
             // wide-node fetches per lane per loop iteration of a sliced walk (A/B
             // on C5: 16 -> 166.1 ms, 20 -> 163.9, 24 -> 163.5, 28 -> 164.4, 32 -> 166.4)
             p.wsteps = (uint32_t)std::max<uint64_t>(1, env_u64("RT_AMD_WSTEPS", 24));
         }
-        p.tbvh_r = tb.radius; p.tbvh_mag = tb.mag;
+        p.tbvh_r = tb.radius; p.tbvh_mag = std::max(tb.mag, w.tcells.mag);
     }
     const float inv_spp = 1.0f / (float)o.samples_per_pixel;  // 1.0 / spp as f32 (common.rs:345)
     p.inv_spp = inv_spp;
@@ -1100,6 +1115,9 @@ static int serial_find_states(WorldState &w, const CameraModel &cam, size_t widt
         bool pixtab = spp >= 4 && env_u64("RT_AMD_SERIAL_PIXTAB", 1) != 0;
         // the pixel pass's per-pixel spans (one load per refill, whole-chunk rows)
         const bool use_spix = env_u64("RT_AMD_SERIAL_SPIX", 1) != 0;
+        // ... and an iteration's reuse of the previous one's table (the positions
+        // both windows cover, after a stop: DESIGN.md 3.4); two tables, alternating
+        const bool reuse = use_spix && env_u64("RT_AMD_SERIAL_REUSE", 1) != 0;
         const uint64_t pchunk = std::max<uint64_t>(1, env_u64("RT_AMD_SERIAL_PCHUNK", 128));
         bool coalesce = false;
         // (iterations of 128 k samples in blocks of 32 for the coalescing search,
@@ -1212,7 +1230,8 @@ static int serial_find_states(WorldState &w, const CameraModel &cam, size_t widt
         const bool pgather = pixtab && env_u64("RT_AMD_SERIAL_PGATHER", 0) != 0;
         if (pixtab) {
             HIP_TRY(grow(d->sptab, d->sptab_cap, npq_max * emax));
-            HIP_TRY(grow(d->sspix, d->sspix_cap, npq_max));
+            HIP_TRY(grow(d->sspix, d->sspix_cap, 2 * npq_max));
+            if (reuse) HIP_TRY(grow(d->sptab2, d->sptab2_cap, npq_max * emax));
             if (pgather) HIP_TRY(grow(d->samples, d->samples_cap, L * K));
         }
         // The walks size each iteration's windows from the per-pixel variances
@@ -1273,9 +1292,11 @@ static int serial_find_states(WorldState &w, const CameraModel &cam, size_t widt
             HIP_TRY(hipMalloc((void **)&d->sjump, jt.size() * 4));
             HIP_TRY(hipMemcpy(d->sjump, jt.data(), jt.size() * 4, hipMemcpyHostToDevice));
         }
-        if (!d->sctrl) HIP_TRY(hipMalloc((void **)&d->sctrl, 32));
-        const uint32_t ctrl0[8] = {0u, o.seed, 0u, 0u, 0u, K0, 0u, 0u};  // Random::new() (random.rs:8-10)
-        HIP_TRY(hipMemcpyAsync(d->sctrl, ctrl0, 32, hipMemcpyHostToDevice, s));
+        if (!d->sctrl) HIP_TRY(hipMalloc((void **)&d->sctrl, 64));
+        // Random::new() (random.rs:8-10); words 8-11: the previous iteration (reuse)
+        const uint32_t ctrl0[16] = {0u, o.seed, 0u, 0u, 0u, K0, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
+        HIP_TRY(hipMemcpyAsync(d->sctrl, ctrl0, 64, hipMemcpyHostToDevice, s));
+        uint64_t iter_q = 0;  // iterations queued (table / span buffers alternate)
         // iterations are queued in batches sized by the expected progress;
         // those queued past the end exit at once (ctrl[0])
         uint32_t ctrl[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -1298,25 +1319,35 @@ static int serial_find_states(WorldState &w, const CameraModel &cam, size_t widt
                 return -5;
             }
             const auto t0 = std::chrono::steady_clock::now();
-            for (uint64_t q = 0; q < it; ++q) {
+            for (uint64_t q = 0; q < it; ++q, ++iter_q) {
+                // this iteration's table and spans, and the previous iteration's
+                // (reuse: the two alternate)
+                const bool odd = reuse && (iter_q & 1u);
+                float *const ptab = odd ? d->sptab2 : d->sptab;
+                float *const ptab_prev = reuse ? (odd ? d->sptab : d->sptab2) : nullptr;
+                uint4 *const spix = d->sspix + (odd ? npq_max : 0);
+                const uint4 *const spix_prev = reuse ? d->sspix + (odd ? 0 : npq_max) : nullptr;
                 // (the pixel table pass's job counters are zeroed by the window kernel)
                 HIP_TRY(launch_serial_window(d->sctrl, d->sjump, d->swin, (uint32_t)wlen, pred, d->slo,
                                              (uint32_t)L, (uint32_t)K, depth, (uint32_t)N,
                                              pixtab ? (uint32_t)spp : 0u, (uint32_t)emax,
                                              pixtab ? d->counter : nullptr, kPixtabParts,
-                                             pixtab && use_spix ? d->sspix : nullptr,
-                                             (uint32_t)pchunk, s));
+                                             pixtab && use_spix ? spix : nullptr,
+                                             (uint32_t)pchunk, spix_prev, s));
                 if (pixtab) {
+                    if (reuse)
+                        HIP_TRY(launch_serial_reuse(d->sctrl, spix, spix_prev, ptab, ptab_prev, (uint32_t)npq_max,
+                                                    (uint32_t)spp, (uint32_t)L, (uint32_t)N, s));
                     SerialPass sp{kRngSerialPixel, 0u, (uint32_t)npq_max, (uint32_t)emax, d->swin, pred, d->sctrl,
                                   d->slo};
-                    sp.ptab = d->sptab;
-                    sp.spix = use_spix ? d->sspix : nullptr;
+                    sp.ptab = ptab;
+                    sp.spix = use_spix ? spix : nullptr;
                     sp.L = (uint32_t)L;
                     sp.Kmax = (uint32_t)K;
                     rc = render_frame(w, cam, width, height, ob, nullptr, s, nullptr, &sp);
                     if (rc) return rc;
                     if (pgather)
-                        HIP_TRY(launch_serial_pixtab_gather(d->sctrl, d->sptab, d->slo, d->samples, (uint32_t)L,
+                        HIP_TRY(launch_serial_pixtab_gather(d->sctrl, ptab, d->slo, d->samples, (uint32_t)L,
                                                            (uint32_t)K, (uint32_t)spp, (uint32_t)N, s));
                 } else {
                     SerialPass sp{coalesce ? kRngSerialCoalesce : kRngSerialCount, 0u, (uint32_t)L, (uint32_t)K,
@@ -1334,7 +1365,7 @@ static int serial_find_states(WorldState &w, const CameraModel &cam, size_t widt
                                            gather ? d->spath : nullptr, gather ? d->sfin : nullptr, d->slo,
                                            d->ssbend, d->ssb, (uint32_t)L, (uint32_t)Lw, (uint32_t)K,
                                            (uint32_t)R_walk, depth, (uint32_t)N,
-                                           (pixtab && !pgather) ? d->sptab : nullptr, walk_lds, s));
+                                           (pixtab && !pgather) ? ptab : nullptr, walk_lds, s));
             }
             const auto t1 = std::chrono::steady_clock::now();
             HIP_TRY(hipMemcpyAsync(ctrl, d->sctrl, 32, hipMemcpyDeviceToHost, s));

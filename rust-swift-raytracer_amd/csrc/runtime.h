@@ -55,6 +55,7 @@ struct DeviceState {
     uint32_t tnodes = 0, ttris = 0, tloose = 0;
     uint4 *tw_nodes = nullptr;                                  // its 4-wide image (bvh.h wnodes)
     uint32_t tw_depth = 0;                                      // stack entries per lane
+    float *tw_tris = nullptr;                                   // per-cell trees' records (tcells)
     uint4 *cam_nodes = nullptr;                                 // camera-origin triangle BVH
     float4 *cam_tris = nullptr;
     uint32_t cam_nnodes = 0;
@@ -91,7 +92,8 @@ struct DeviceState {
     uint32_t *sbend = nullptr;       size_t sbend_cap = 0;
     uint32_t *spath = nullptr;       size_t spath_cap = 0;  // block walks' paths (L x K)
     float *sptab = nullptr;          size_t sptab_cap = 0;  // pixel table pass: b per (pixel, position)
-    uint2 *sspix = nullptr;          size_t sspix_cap = 0;  // pixel table pass: {plo, phi} per pixel
+    uint4 *sspix = nullptr;          size_t sspix_cap = 0;  // pixel table pass: spans per pixel, 2 buffers
+    float *sptab2 = nullptr;         size_t sptab2_cap = 0; // (the previous iteration's table: reuse)
     uint32_t *sfin = nullptr;                               // chain result (4 + kMaxWalkBlocks)
     uint32_t *sjump = nullptr;
     uint32_t *sctrl = nullptr;
@@ -131,6 +133,7 @@ struct WorldState {
     PackedScene packed;
     SphereBVH bvh;
     TriangleBVH tbvh;
+    TriangleCells tcells;  // per-origin-cell trees (RT_AMD_TRI_CELLS), usually empty
     CameraTriangleBVH ctree;      // for the camera origin of ctree_version
     uint64_t ctree_version = 0;   // 0: none built
     bool ctree_full = false;      // ctree has its nodes (else records only)
@@ -174,7 +177,7 @@ struct SerialPass {
     // positions, the launch's bounds), the iteration length and its K
     float *ptab = nullptr;
     uint32_t L = 0, Kmax = 0;
-    const uint2 *spix = nullptr;  // its pixels' position spans (serial_window_kernel)
+    const uint4 *spix = nullptr;  // its pixels' position spans (serial_window_kernel)
 };
 
 // Renders rank's tile of a width x height frame into device memory d_out

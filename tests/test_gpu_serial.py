@@ -125,6 +125,38 @@ def test_serial_narrow_windows_and_short_iterations(monkeypatch):
             monkeypatch.delenv(k)
 
 
+def test_serial_table_reuse_after_stops(monkeypatch):
+    """Windows forced narrow (K = 24 / 30 candidates) so that most pixel-table
+    iterations stop short: each next iteration copies the entries of the
+    stopped one's table that its own windows cover (serial_reuse_kernel) and
+    traces only the rest.  Bit-exact against the oracle's SERIAL frame, and
+    the same iterations, stops and frame with the reuse switched off and
+    without the per-pixel spans (RT_AMD_SERIAL_SPIX=0: no chunk skipping
+    either); odd job chunks (rows padded to 7 and 1000 positions)."""
+    for scene, size, env in [
+        ("c_raytracer_world.txt", (80, 60, 16, 8), dict(RT_AMD_SERIAL_K="24", RT_AMD_SERIAL_CHUNK="512")),
+        ("world.txt", (48, 27, 16, 8), dict(RT_AMD_SERIAL_K="30", RT_AMD_SERIAL_CHUNK="2000")),
+        ("world.txt", (40, 30, 8, 8), dict(RT_AMD_SERIAL_K="24", RT_AMD_SERIAL_CHUNK="700",
+                                           RT_AMD_SERIAL_PCHUNK="7")),
+        ("c_raytracer_world.txt", (40, 30, 16, 8), dict(RT_AMD_SERIAL_K="30", RT_AMD_SERIAL_CHUNK="900",
+                                                       RT_AMD_SERIAL_PCHUNK="1000")),
+    ]:
+        img, st, _ = O.Scene(scene_text(scene)).render(*size, mode=O.RNG_SERIAL)
+        runs = {}
+        for label, extra in (("reuse", {}), ("off", dict(RT_AMD_SERIAL_REUSE="0")),
+                             ("nospix", dict(RT_AMD_SERIAL_SPIX="0"))):
+            for k, v in {**env, **extra}.items():
+                monkeypatch.setenv(k, v)
+            out, gst = R.World(scene_text(scene)).render(*size, mode=R.RNG_SERIAL)
+            for k in {**env, **extra}:
+                monkeypatch.delenv(k)
+            assert_bits_equal(out, img, f"SERIAL frame {scene} {size} {env} {label}")
+            assert gst["rays"] == st["rays"]
+            runs[label] = (gst["serial_iterations"], gst["serial_retries"])
+        assert runs["reuse"] == runs["off"] == runs["nospix"], runs
+        assert runs["reuse"][1] > runs["reuse"][0] // 4, runs  # most iterations stop short
+
+
 SEARCHES = {
     # runtime.cpp serial_find_states: the pixel table (default from 4 spp), the
     # count pass + block walks, the coalescing block search
