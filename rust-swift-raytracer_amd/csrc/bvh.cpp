@@ -617,6 +617,28 @@ void build_wide_image(TriangleBVH &tb) {
     }
 }
 
+float triangle_cell_edge(const std::vector<Triangle> &tris, uint32_t max_cells) {
+    double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+    for (const Triangle &t : tris)
+        for (const Vec3 &v : {t.v0, t.v1, t.v2}) {
+            const double c[3] = {v.x, v.y, v.z};
+            if (!(std::isfinite(c[0]) && std::isfinite(c[1]) && std::isfinite(c[2]))) continue;
+            for (int k = 0; k < 3; ++k) { lo[k] = std::min(lo[k], c[k]); hi[k] = std::max(hi[k], c[k]); }
+        }
+    double ext = 0;
+    for (int k = 0; k < 3; ++k) {
+        if (!(lo[k] <= hi[k])) return 0.0f;
+        ext = std::max(ext, hi[k] - lo[k]);
+    }
+    if (!(ext > 0) || !std::isfinite(ext)) return 0.0f;
+    for (double s = ext / 64; s <= ext * 2; s *= 1.05) {
+        double n = 1;
+        for (int k = 0; k < 3; ++k) n *= std::max(1.0, std::ceil((hi[k] - (double)(float)lo[k]) / s + 1e-9));
+        if (n <= max_cells) return (float)s;
+    }
+    return (float)ext;
+}
+
 TriangleCells build_triangle_cells(const std::vector<Triangle> &tris, const std::vector<float> &tri_hot,
                                    uint32_t leaf_size, float size, TriangleBVH &tb) {
     TriangleCells out;
@@ -640,7 +662,10 @@ TriangleCells build_triangle_cells(const std::vector<Triangle> &tris, const std:
     out.size = size;
     out.ncells = (uint32_t)ncells;
     // one tree per cell, on host threads (SAH scale: the cell's half-diagonal,
-    // as the emulation, tools/tbvh_sim.cpp SIM_CELL)
+    // as the emulation, tools/tbvh_sim.cpp SIM_CELL).  Every cell gets its own
+    // tree: the kernel widens from the centre of the origin's cell, so a cell's
+    // slot must hold the tree built for that centre (a copy of the static tree
+    // there made frames wrong in a first try)
     std::vector<TriangleBVH> trees(ncells);
     std::atomic<uint64_t> next{0};
     auto work = [&]() {
@@ -659,13 +684,15 @@ TriangleCells build_triangle_cells(const std::vector<Triangle> &tris, const std:
     // one grid for every tree (and the static one): the union of their roots
     float glo[3], ghi[3];
     for (int k = 0; k < 3; ++k) { glo[k] = tb.nodes[k]; ghi[k] = tb.nodes[4 + k]; }
-    for (const TriangleBVH &t : trees) {
+    for (uint64_t c = 0; c < ncells; ++c) {
+        const TriangleBVH &t = trees[c];
         if (t.nodes.empty() || t.wnodes.empty()) return TriangleCells{};
         for (int k = 0; k < 3; ++k) { glo[k] = std::min(glo[k], t.nodes[k]); ghi[k] = std::max(ghi[k], t.nodes[4 + k]); }
     }
     trees.push_back(tb);
     uint64_t sw = 0, sr = 0;
-    for (TriangleBVH &t : trees) {
+    for (uint64_t c = 0; c <= ncells; ++c) {
+        TriangleBVH &t = trees[c];
         quantize_boxes(t.nodes, 16, true, t.miss, t.qnodes, t.qbox, &t.nbase, &t.nstep, glo, ghi);
         build_wide_image(t);
         if (t.wnodes.empty()) return TriangleCells{};
@@ -680,8 +707,9 @@ TriangleCells build_triangle_cells(const std::vector<Triangle> &tris, const std:
     out.wnodes.assign((ncells + 1) * sw * 32, 0u);
     out.tris.assign((ncells + 1) * sr * 16, 0.0f);
     for (uint64_t c = 0; c <= ncells; ++c) {
-        std::copy(trees[c].wnodes.begin(), trees[c].wnodes.end(), out.wnodes.begin() + c * sw * 32);
-        std::copy(trees[c].tris.begin(), trees[c].tris.end(), out.tris.begin() + c * sr * 16);
+        const TriangleBVH &t = trees[c];
+        std::copy(t.wnodes.begin(), t.wnodes.end(), out.wnodes.begin() + c * sw * 32);
+        std::copy(t.tris.begin(), t.tris.end(), out.tris.begin() + c * sr * 16);
     }
     tb = trees.back();  // (the static tree on the common grid: its binary walk's nodes too)
     return out;

@@ -116,6 +116,9 @@ struct TriangleCells {
 // the kernel's 32-bit indices.
 TriangleCells build_triangle_cells(const std::vector<Triangle> &tris, const std::vector<float> &tri_hot,
                                    uint32_t leaf_size, float size, TriangleBVH &tb);
+// The smallest cell edge (of a geometric ladder) that cuts the box of the
+// mesh's finite vertices into at most max_cells cells; 0 for an empty mesh.
+float triangle_cell_edge(const std::vector<Triangle> &tris, uint32_t max_cells);
 
 // tri_hot: PackedScene::tri_hot (the exact per-triangle n and n.v0 bits).
 // oc (optional): origin the boxes are built for; phantom: SAH weight of the

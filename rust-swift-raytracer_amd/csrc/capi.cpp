@@ -77,17 +77,26 @@ Rust_WorldHandle *load_world(const char *source) {
     world->state.tbvh = rtamd::build_triangle_bvh(world->state.scene.triangles,
                                                   world->state.packed.tri_hot,
                                                   env_leaf("RT_AMD_TRI_LEAF", 1u));
-    // per-origin-cell trees, RT_AMD_TRI_CELLS=<cell edge> (measured and left
-    // off): the static tree is re-quantised on their common grid
-    if (const char *cs = std::getenv("RT_AMD_TRI_CELLS")) {
-        const float size = std::strtof(cs, nullptr);
+    // per-origin-cell trees: for meshes of >= 64 k triangles
+    // by default, cells of the edge that cuts the mesh's box into <= 32 (A/B on
+    // C5, profiles/round6_c5_cells: static tree 147.1 ms; 1.5 / 2 / 2.5-unit cells,
+    // 124 / 56 / 30 trees: 142.5 / 140.0 / 139.5 ms; 3 / 4-unit cells 145.4 /
+    // 149.3 ms); RT_AMD_TRI_CELLS=<edge> sets the edge, 0 switches them off.
+    // The static tree is re-quantised on their common grid.
+    {
+        float size = 0.0f;
+        if (const char *cs = std::getenv("RT_AMD_TRI_CELLS")) {
+            size = std::strtof(cs, nullptr);
+        } else if (world->state.scene.triangles.size() >= 65536 && !world->state.tbvh.nodes.empty()) {
+            size = rtamd::triangle_cell_edge(world->state.scene.triangles, 32);
+        }
         if (size > 0.0f)
             world->state.tcells = rtamd::build_triangle_cells(world->state.scene.triangles,
                                                               world->state.packed.tri_hot,
                                                               env_leaf("RT_AMD_TRI_LEAF", 1u), size,
                                                               world->state.tbvh);
         const auto &tc = world->state.tcells;
-        std::fprintf(stderr, "tri cells: %u x %u x %u = %u cells of %.3g, %u wide nodes and %u records per tree, "
+        if (std::getenv("RT_AMD_TRI_CELLS_DEBUG")) std::fprintf(stderr, "tri cells: %u x %u x %u = %u cells of %.3g, %u wide nodes and %u records per tree, "
                      "%.1f MB\n", tc.n[0], tc.n[1], tc.n[2], tc.ncells, tc.size, tc.stride_w, tc.stride_r,
                      (tc.wnodes.size() * 4.0 + tc.tris.size() * 4.0) / 1e6);
     }
