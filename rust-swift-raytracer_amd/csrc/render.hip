@@ -1313,13 +1313,12 @@ void trace_kernel(TraceParams p) {
                 // picks the same tree.  Any tree is exact for any origin: the
                 // widening below covers o - oc (bvh.h TriangleCells).
                 F3 oc = f3(p.tbvh_oc[0], p.tbvh_oc[1], p.tbvh_oc[2]);
-                uint32_t wbase = 0;
-                const float4 *wrecs = nullptr;
+                uint32_t tree = 0;  // (one register across the walk: the bases follow from it)
                 if (p.tc_ncells != 0u) {
                     const float fx = floorf((org.x - p.tc_lo[0]) * p.tc_inv_size);
                     const float fy = floorf((org.y - p.tc_lo[1]) * p.tc_inv_size);
                     const float fz = floorf((org.z - p.tc_lo[2]) * p.tc_inv_size);
-                    uint32_t tree = p.tc_ncells;
+                    tree = p.tc_ncells;
                     if (fx >= 0.0f && fx < (float)p.tc_n[0] && fy >= 0.0f && fy < (float)p.tc_n[1] && fz >= 0.0f &&
                         fz < (float)p.tc_n[2]) {
                         tree = ((uint32_t)fz * p.tc_n[1] + (uint32_t)fy) * p.tc_n[0] + (uint32_t)fx;
@@ -1327,8 +1326,6 @@ void trace_kernel(TraceParams p) {
                         oc = f3(p.tc_lo[0] + (fx + 0.5f) * p.tc_size, p.tc_lo[1] + (fy + 0.5f) * p.tc_size,
                                 p.tc_lo[2] + (fz + 0.5f) * p.tc_size);
                     }
-                    wbase = tree * p.tw_stride;
-                    wrecs = p.tw_tris + (size_t)4u * tree * p.tw_rstride;
                 }
                 const F3 dlt2 = f3(2.0f * (org.x - oc.x), 2.0f * (org.y - oc.y), 2.0f * (org.z - oc.z));
                 F3 nlo, nhi;
@@ -1340,7 +1337,7 @@ void trace_kernel(TraceParams p) {
                          __builtin_fmaf(p.tq_base[2], inv.z, nhi.z));
                 float cap = fminf(best_t, tri_t);
                 do {
-                    const uint4 *wn = p.tw_nodes + 8u * (wbase + node);
+                    const uint4 *wn = p.tw_nodes + 8u * (tree * p.tw_stride + node);
                     tnode_tests += 4;
                     float tn[4];
                     bool in[4];
@@ -1379,7 +1376,7 @@ void trace_kernel(TraceParams p) {
                         lmask &= lmask - 1u;
                         const uint32_t lw = c == 0 ? a[0] : c == 1 ? a[1] : c == 2 ? a[2] : a[3];
                         tri_leaf(p, org, dir, false, lw & ~kLeafBitDev, best_t, tri_t, tri_i, tri_in, tri_done,
-                                 wrecs);
+                                 p.tc_ncells != 0u ? p.tw_tris + (size_t)4u * tree * p.tw_rstride : nullptr);
                     }
                     cap = fminf(best_t, tri_t);
                     uint32_t nxt = 0xFFFFu;
