@@ -179,3 +179,39 @@ def test_serial_multi_device_path_one_device():
     assert_bits_equal(out, img, "ndevices=1 SERIAL frame")
     assert gst["rays"] == st["rays"] and gst["serial_chain_breaks"] == 0 and gst["serial_checked"] == 48 * 40 * 4
     assert gst["serial_ms"] > 0
+
+
+def test_job_counter_sets_across_streams_serial_and_partitions(monkeypatch):
+    """The double-buffered job counters (runtime.cpp: a frame launch takes one
+    set, zeroed by the launch before it, and zeroes the other): COUNTER frames
+    on a user stream and on the library stream, a SERIAL frame (whose passes
+    reset the sets) between them, and the partition count changed from frame
+    to frame (RT_AMD_PARTS 1, 1024, 3, default).  Every frame's bits and
+    ray / sample counts equal the first frame's."""
+    import torch
+
+    src = scene_text("rtow.txt")
+    w, h, spp = 120, 68, 8
+    world = R.World(src)
+    ref, st0 = world.render(w, h, spp, 8)
+    frame = torch.zeros(w * h * 4, dtype=torch.uint8, device="cuda:0")
+    user = torch.cuda.Stream(device="cuda:0")
+    serial_ref, _, _ = O.Scene(src).render(w // 4, h // 4, 4, 8, mode=O.RNG_SERIAL)
+    for k, parts in enumerate(["1", "1024", "3", None, "1024", "1"]):
+        if parts is None:
+            monkeypatch.delenv("RT_AMD_PARTS", raising=False)
+        else:
+            monkeypatch.setenv("RT_AMD_PARTS", parts)
+        if k % 2 == 0:  # a user stream (rt_render_device), counted and uncounted
+            st = world.render_device(w, h, frame.data_ptr(), user.cuda_stream, spp=spp, depth=8, device=0)
+            world.render_device(w, h, frame.data_ptr(), user.cuda_stream, spp=spp, depth=8, device=0,
+                                stats=False)
+            user.synchronize()
+            out = frame.cpu().numpy().reshape(h, w, 4)
+        else:  # the library stream
+            out, st = world.render(w, h, spp, 8)
+        assert_bits_equal(out, ref, f"frame {k} (RT_AMD_PARTS={parts})")
+        assert st["rays"] == st0["rays"] and st["samples"] == st0["samples"], (k, st, st0)
+        if k in (1, 3):  # a SERIAL frame between COUNTER frames
+            sout, _ = world.render(w // 4, h // 4, 4, 8, mode=R.RNG_SERIAL)
+            assert_bits_equal(sout, serial_ref, f"SERIAL frame after frame {k}")

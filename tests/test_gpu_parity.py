@@ -491,6 +491,27 @@ def test_triangle_bvh_equals_brute_force(case):
     assert sb["tri_in_range"] <= sa["tri_in_range"]
 
 
+@pytest.mark.parametrize("edge", ["1.3", "2.5", "4"])
+@pytest.mark.parametrize("case", [
+    dict(seed=12, n=400, size=2.0, dup=80, slivers=30),
+    dict(seed=13, n=300, spheres=200, grid=12),
+    dict(seed=15, n=400, offset=(2500.0, -1800.0, 900.0), cam=(2500.0, -1800.0, 900.0)),
+    dict(seed=16, n=400, cam=(0.0, 0.0, -6.0), size=1.0),
+])
+def test_triangle_cell_trees_equal_brute_force(monkeypatch, case, edge):
+    """Per-origin-cell triangle trees (bvh.h TriangleCells; on by default only
+    for meshes of >= 64k triangles) forced onto small soups at three cell
+    edges: every sample equals brute force, whichever cell tree (or the static
+    tree, for origins outside every cell) a ray walks."""
+    monkeypatch.setenv("RT_AMD_TRI_CELLS", edge)
+    src = _triangle_scene(**case)
+    a, sa, sma, b, sb, smb = _both_modes(src, 64, 48, 8)
+    assert sb["tri_bvh"] == 1
+    assert_bits_equal(b, a, "frame")
+    assert_bits_equal(smb[:, :3], sma[:, :3], "samples")
+    assert sa["rays"] == sb["rays"]
+
+
 def test_triangle_bvh_matches_oracle():
     src = _triangle_scene(21, 300, size=1.0, slivers=10, dup=20, spheres=50)
     img, st, _, smp = O.Scene(src).render(48, 32, 4, 8, mode=O.RNG_COUNTER, nthreads=8,
