@@ -661,6 +661,9 @@ TriangleCells build_triangle_cells(const std::vector<Triangle> &tris, const std:
     if (ncells > 4096) return out;
     out.size = size;
     out.ncells = (uint32_t)ncells;
+    // (RT_AMD_TRI_CELL_SAH: the SAH phantom scale in half-diagonals, tuning only)
+    const char *sah_env = std::getenv("RT_AMD_TRI_CELL_SAH");
+    const double sah = sah_env ? std::max(1e-3, std::atof(sah_env)) : 1.0;
     // one tree per cell, on host threads (SAH scale: the cell's half-diagonal,
     // as the emulation, tools/tbvh_sim.cpp SIM_CELL).  Every cell gets its own
     // tree: the kernel widens from the centre of the origin's cell, so a cell's
@@ -673,7 +676,7 @@ TriangleCells build_triangle_cells(const std::vector<Triangle> &tris, const std:
             const uint64_t x = c % out.n[0], y = (c / out.n[0]) % out.n[1], z = c / (out.n[0] * out.n[1]);
             const float oc[3] = {out.lo[0] + ((float)x + 0.5f) * size, out.lo[1] + ((float)y + 0.5f) * size,
                                  out.lo[2] + ((float)z + 0.5f) * size};
-            trees[c] = build_triangle_bvh(tris, tri_hot, leaf_size, oc, size * 0.866);
+            trees[c] = build_triangle_bvh(tris, tri_hot, leaf_size, oc, size * 0.866 * sah);
         }
     };
     const unsigned nt = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));

@@ -2243,7 +2243,9 @@ __global__ __launch_bounds__(kWalkLdsThreads) void serial_walk_blocks_lds_kernel
         uint32_t plo = w.plo[0], span = w.span[0], off = w.off[0];
         uint32_t jl = j0;
         for (; jl < j1; ++jl) {
+#ifndef RT_DIAG_NO_PATH  // (timing-only diagnostic build: no path records, wrong states)
             path[(size_t)(jl - j0) * stride + t] = B;
+#endif
             if (jl == jnext) {
                 ++i;
                 jnext += spp;

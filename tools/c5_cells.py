@@ -19,14 +19,20 @@ make, W, H, spp, depth = S.CONFIGS["c5"]
 src = make()
 worlds = {}
 for cs in ["off"] + sys.argv[1:]:
+    # "edge[:sah]": the cell edge and the cell trees' SAH phantom scale
+    os.environ.pop("RT_AMD_TRI_CELL_SAH", None)
     if cs == "off":
-        os.environ.pop("RT_AMD_TRI_CELLS", None)
+        os.environ["RT_AMD_TRI_CELLS"] = "0"
     else:
-        os.environ["RT_AMD_TRI_CELLS"] = cs
+        edge, _, sah = cs.partition(":")
+        os.environ["RT_AMD_TRI_CELLS"] = edge
+        if sah:
+            os.environ["RT_AMD_TRI_CELL_SAH"] = sah
     t = time.perf_counter()
     worlds[cs] = R.World(src)
     print(cs, "load %.1f s" % (time.perf_counter() - t), flush=True)
 os.environ.pop("RT_AMD_TRI_CELLS", None)
+os.environ.pop("RT_AMD_TRI_CELL_SAH", None)
 torch.cuda.set_device(0)
 out = torch.zeros(W * H * 4, dtype=torch.uint8, device="cuda")
 stream = torch.cuda.current_stream()

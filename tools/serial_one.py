@@ -14,7 +14,8 @@ import scenes as S  # noqa: E402
 for case in sys.argv[1:]:
     sc, dims = case.split(":")
     W, H, spp = (int(x) for x in dims.split("x"))
-    w = R.World(S.read("world.txt") if sc == "world" else S.read("c_raytracer_world.txt") if sc == "c_raytracer" else S.rtow())
+    w = R.World(S.read("world.txt") if sc == "world" else S.read("c_raytracer_world.txt") if sc == "c_raytracer" else S.rtow(),
+                lib_path=os.environ.get("RT_LIB") or None)
     t = time.perf_counter()
     _, st = w.render(W, H, spp, 8, mode=R.RNG_SERIAL)
     print(case, "wall %.1f ms" % ((time.perf_counter() - t) * 1e3), "search %.1f ms" % st["serial_ms"],
