@@ -506,9 +506,9 @@ def _report(args, src, world, W, H, spp, depth, st0, rays, elapsed, trace_ms, co
     ms_per_step = elapsed / args.steps * 1e3
     # VALU evidence of the same hash-keyed profile (tools/pmc_summary.py): lanes
     # active per VALU instruction, VALU lane-slots per ray and the issue rate
-    # against the v_add_f32 microbenchmark (tools/ubench_valu on the box,
-    # profiles/valu_ceiling.json) -- null unless the profiled trace kernel is
-    # the one this run loaded
+    # against the v_add_f32 issue rate measured on the box
+    # (tools/probe/ubench_enc.hip, profiles/valu_ceiling.json) -- null unless
+    # the profiled trace kernel is the one this run loaded
     same = bool(tsrc and tsrc["same_trace_kernel"])
     pv = (ent.get("valu") or {}) if same else {}
     ceiling = None
