@@ -661,11 +661,14 @@ TriangleCells build_triangle_cells(const std::vector<Triangle> &tris, const std:
     if (ncells > 4096) return out;
     out.size = size;
     out.ncells = (uint32_t)ncells;
-    // (RT_AMD_TRI_CELL_SAH: the SAH phantom scale in half-diagonals, tuning only)
+    // SAH phantom scale in half-diagonals (RT_AMD_TRI_CELL_SAH, tuning only):
+    // 0.4, between the two best measured scales (a uniform origin lies 0.55
+    // half-diagonals from its cell's centre on average).  C5 lean frames at 2.5-unit cells
+    // (profiles/round6_c5_cells/sah_scale_sweep*.log): scale 1e-3 148.1 ms,
+    // 0.25 135.1, 0.5 135.3, 1 138.7, 2 145.7, 4 167.8
     const char *sah_env = std::getenv("RT_AMD_TRI_CELL_SAH");
-    const double sah = sah_env ? std::max(1e-3, std::atof(sah_env)) : 1.0;
-    // one tree per cell, on host threads (SAH scale: the cell's half-diagonal,
-    // as the emulation, tools/tbvh_sim.cpp SIM_CELL).  Every cell gets its own
+    const double sah = sah_env ? std::max(1e-3, std::atof(sah_env)) : 0.4;
+    // one tree per cell, on host threads.  Every cell gets its own
     // tree: the kernel widens from the centre of the origin's cell, so a cell's
     // slot must hold the tree built for that centre (a copy of the static tree
     // there made frames wrong in a first try)
