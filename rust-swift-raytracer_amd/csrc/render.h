@@ -137,13 +137,6 @@ struct TraceParams {
     const uint4 *tw_nodes;    // 8 per wide node (128 B)
     uint32_t tw_depth;        // stack entries per lane (3 * TriangleBVH::wdepth, >= 1)
     uint32_t wsteps;          // wide-node fetches per lane per loop iteration (sliced walks)
-    // per-origin-cell trees (bvh.h TriangleCells; tc_ncells == 0: the static
-    // tree only): tree c's wide nodes from tw_nodes + 8 c tw_stride, its records
-    // from tw_tris + 4 c tw_rstride; tree tc_ncells is the static tree
-    const float4 *tw_tris;
-    uint32_t tw_stride, tw_rstride, tc_ncells;
-    uint32_t tc_n[3];
-    float tc_lo[3], tc_size, tc_inv_size;
     float cq_base[3], cq_step[3];                      // camera-tree grid
     // the same triangles' phantoms for the camera origin (bvh.h CameraTriangleBVH),
     // used at bounce 0; cam_nnodes == 0: bounce 0 uses the tree above
@@ -175,16 +168,25 @@ struct TraceParams {
     FastDiv div_sspp;         // ... and its divider
     uint32_t max_draws;       // 2 + 3 * max(depth, 0): bound of the draw count search
     uint32_t sL, sK;          // kRngSerialPixel: the iteration length and the launch's K
-    const uint4 *spix;        // kRngSerialPixel (optional): per local pixel its positions
-                              // {plo, phi} and the positions [z, w] (relative to plo; empty
-                              // when z > w) copied from the previous iteration's table
-                              // (serial_window_kernel, serial_reuse_kernel): not traced
     // frames of one rank whose global job indices (row * W + col) * spp + s
     // fit 32 bits (gj32 != 0): the global job of launch job j in local row q is
     // j + gj_c0 - q * gj_2p (mod 2^32), gj_c0 = (H - 1 - slab_row0) W spp,
     // gj_2p = 2 W spp -- the refill's job -> (pixel, seed) without the
     // row-block map and the 64-bit products
     uint32_t gj32, gj_c0, gj_2p;
+    // (round-6 fields last: the offsets of the fields above stay those the
+    // frame kernels' kernarg loads were tuned with)
+    // per-origin-cell trees (bvh.h TriangleCells; tc_ncells == 0: the static
+    // tree only): tree c's wide nodes from tw_nodes + 8 c tw_stride, its records
+    // from tw_tris + 4 c tw_rstride; tree tc_ncells is the static tree
+    const float4 *tw_tris;
+    uint32_t tw_stride, tw_rstride, tc_ncells;
+    uint32_t tc_n[3];
+    float tc_lo[3], tc_size, tc_inv_size;
+    const uint4 *spix;        // kRngSerialPixel (optional): per local pixel its positions
+                              // {plo, phi} and the positions [z, w] (relative to plo; empty
+                              // when z > w) copied from the previous iteration's table
+                              // (serial_window_kernel, serial_reuse_kernel): not traced
 };
 
 // Candidate k of chunk sample jl (frame sample a + jl) means B = serial_lo + k

@@ -1636,8 +1636,10 @@ void trace_kernel(TraceParams p) {
                         cur_off = (k << pc.ring_shift) - base;
                     }
                 }
+                if (!kSerial) break;  // (frames: one pass, as the plain `if` it replaces)
             }
-            const uint32_t avail = exhausted ? 0u : pool_end - pool_next;
+            // (the pixel pass's skipped chunks may leave pool_end below pool_next)
+            const uint32_t avail = kSerial && exhausted ? 0u : pool_end - pool_next;
             const uint32_t rank = __builtin_amdgcn_mbcnt_hi(
                 (uint32_t)(dead >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)dead, 0u));
             if (!active && rank < avail) {
