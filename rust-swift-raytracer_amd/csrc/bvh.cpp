@@ -696,27 +696,55 @@ TriangleCells build_triangle_cells(const std::vector<Triangle> &tris, const std:
         for (int k = 0; k < 3; ++k) { glo[k] = std::min(glo[k], t.nodes[k]); ghi[k] = std::max(ghi[k], t.nodes[4 + k]); }
     }
     trees.push_back(tb);
-    uint64_t sw = 0, sr = 0;
+    uint64_t sw = 0;
     for (uint64_t c = 0; c <= ncells; ++c) {
         TriangleBVH &t = trees[c];
         quantize_boxes(t.nodes, 16, true, t.miss, t.qnodes, t.qbox, &t.nbase, &t.nstep, glo, ghi);
         build_wide_image(t);
         if (t.wnodes.empty()) return TriangleCells{};
         sw = std::max<uint64_t>(sw, t.wnodes.size() / 32);
-        sr = std::max<uint64_t>(sr, t.tris.size() / 16);
         out.wdepth = std::max(out.wdepth, t.wdepth);
         out.mag = std::max(out.mag, t.mag);
     }
-    if ((ncells + 1) * sw >= (1ull << 32) || (ncells + 1) * sr * 4 >= (1ull << 32)) return TriangleCells{};
-    out.stride_w = (uint32_t)sw;
-    out.stride_r = (uint32_t)sr;
-    out.wnodes.assign((ncells + 1) * sw * 32, 0u);
-    out.tris.assign((ncells + 1) * sr * 16, 0.0f);
-    for (uint64_t c = 0; c <= ncells; ++c) {
-        const TriangleBVH &t = trees[c];
-        std::copy(t.wnodes.begin(), t.wnodes.end(), out.wnodes.begin() + c * sw * 32);
-        std::copy(t.tris.begin(), t.tris.end(), out.tris.begin() + c * sr * 16);
+    if ((ncells + 1) * sw >= (1ull << 32)) return TriangleCells{};
+    // One record array for every tree.  A record holds nothing of its tree
+    // ((n, n.v0) (v0, id) (v1) (v2), triangle_records), so the static tree's
+    // records serve all of them: a cell tree's leaf is pointed at its
+    // triangles' run there, and only a leaf whose triangles are not one run
+    // in the static order gets copies appended.  (Per-tree copies took 10 MB
+    // per tree: 30 trees pushed C5's records out of the caches.)
+    const TriangleBVH &st = trees[ncells];
+    auto rec_id = [](const std::vector<float> &r, size_t j) {
+        uint32_t id;
+        std::memcpy(&id, &r[j * 16 + 7], 4);
+        return id;
+    };
+    std::vector<uint32_t> spos(tris.size(), ~0u);
+    for (size_t j = 0; j < st.tris.size() / 16; ++j) spos[rec_id(st.tris, j)] = (uint32_t)j;
+    out.tris = st.tris;
+    for (uint64_t c = 0; c < ncells; ++c) {
+        TriangleBVH &t = trees[c];
+        for (size_t w = 0; w < t.wnodes.size() / 32; ++w)
+            for (int k = 0; k < 4; ++k) {
+                uint32_t &word = t.wnodes[w * 32 + 24 + k];
+                if (!(word & kLeafBit) || (word & 7u) == 0) continue;  // inner / empty child
+                const uint32_t first = (word & ~kLeafBit) >> 3, count = word & 7u;
+                uint32_t s0 = spos[rec_id(t.tris, first)];
+                bool run = s0 != ~0u;
+                for (uint32_t j = 1; run && j < count; ++j) run = spos[rec_id(t.tris, first + j)] == s0 + j;
+                if (!run) {
+                    s0 = (uint32_t)(out.tris.size() / 16);
+                    out.tris.insert(out.tris.end(), t.tris.begin() + (size_t)first * 16,
+                                    t.tris.begin() + (size_t)(first + count) * 16);
+                }
+                if (s0 >= (1u << 28)) return TriangleCells{};  // the leaf word's first field
+                word = kLeafBit | (s0 << 3) | count;
+            }
     }
+    out.stride_w = (uint32_t)sw;
+    out.wnodes.assign((ncells + 1) * sw * 32, 0u);
+    for (uint64_t c = 0; c <= ncells; ++c)
+        std::copy(trees[c].wnodes.begin(), trees[c].wnodes.end(), out.wnodes.begin() + c * sw * 32);
     tb = trees.back();  // (the static tree on the common grid: its binary walk's nodes too)
     return out;
 }

@@ -100,16 +100,17 @@ void build_wide_image(TriangleBVH &tb);
 // origin (the per-ray widening covers o - oc), so the choice of tree only
 // changes the work.  All trees share one quantisation grid (the union of their
 // root boxes; the static tree tb is re-quantised on it), so the kernel's grid
-// parameters stay per launch.  Wide images and records are concatenated with
-// fixed strides (wide nodes, records).
+// parameters stay per launch.  Wide images are concatenated with a fixed
+// stride; the records are one array for all trees (the static tree's, then
+// copies for cell-tree leaves that are not one run of it).
 struct TriangleCells {
     float lo[3] = {0, 0, 0};
     float size = 0;
     uint32_t n[3] = {0, 0, 0};
     uint32_t ncells = 0;
     std::vector<uint32_t> wnodes;   // (ncells + 1) x stride_w wide nodes of 32 u32
-    std::vector<float> tris;        // (ncells + 1) x stride_r records of 16 floats
-    uint32_t stride_w = 0, stride_r = 0, wdepth = 0;
+    std::vector<float> tris;        // records of 16 floats (static tree's first)
+    uint32_t stride_w = 0, wdepth = 0;
     float mag = 0;                  // largest |coordinate| over the trees (rho)
 };
 // Empty (ncells == 0) when a tree has no wide image or the trees do not fit

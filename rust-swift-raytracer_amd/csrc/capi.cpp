@@ -96,8 +96,8 @@ Rust_WorldHandle *load_world(const char *source) {
                                                               env_leaf("RT_AMD_TRI_LEAF", 1u), size,
                                                               world->state.tbvh);
         const auto &tc = world->state.tcells;
-        if (std::getenv("RT_AMD_TRI_CELLS_DEBUG")) std::fprintf(stderr, "tri cells: %u x %u x %u = %u cells of %.3g, %u wide nodes and %u records per tree, "
-                     "%.1f MB\n", tc.n[0], tc.n[1], tc.n[2], tc.ncells, tc.size, tc.stride_w, tc.stride_r,
+        if (std::getenv("RT_AMD_TRI_CELLS_DEBUG")) std::fprintf(stderr, "tri cells: %u x %u x %u = %u cells of %.3g, %u wide nodes per tree, %zu records, "
+                     "%.1f MB\n", tc.n[0], tc.n[1], tc.n[2], tc.ncells, tc.size, tc.stride_w, tc.tris.size() / 16,
                      (tc.wnodes.size() * 4.0 + tc.tris.size() * 4.0) / 1e6);
     }
     // bounce-0 triangle tree for the scene camera (rebuilt by the first render

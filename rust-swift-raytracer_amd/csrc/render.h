@@ -177,10 +177,11 @@ struct TraceParams {
     // (round-6 fields last: the offsets of the fields above stay those the
     // frame kernels' kernarg loads were tuned with)
     // per-origin-cell trees (bvh.h TriangleCells; tc_ncells == 0: the static
-    // tree only): tree c's wide nodes from tw_nodes + 8 c tw_stride, its records
-    // from tw_tris + 4 c tw_rstride; tree tc_ncells is the static tree
+    // tree only): tree c's wide nodes from tw_nodes + 8 c tw_stride; tree
+    // tc_ncells is the static tree.  tw_tris: the records every wide walk's
+    // leaves index (all trees share one array; tbvh_tris without cells)
     const float4 *tw_tris;
-    uint32_t tw_stride, tw_rstride, tc_ncells;
+    uint32_t tw_stride, tc_ncells;
     uint32_t tc_n[3];
     float tc_lo[3], tc_size, tc_inv_size;
     const uint4 *spix;        // kRngSerialPixel (optional): per local pixel its positions

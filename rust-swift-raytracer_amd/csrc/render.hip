@@ -645,7 +645,7 @@ __device__ __forceinline__ bool tri_wide_child(const TraceParams &p, uint32_t w0
 __device__ __forceinline__ void tri_leaf(const TraceParams &p, F3 org, F3 dir, bool cam,
                                          uint32_t leaf, float best_t, float &tri_t, int &tri_i,
                                          uint32_t &tri_in, uint32_t &tri_done, const float4 *wrecs = nullptr) {
-    // (wrecs: the per-cell tree's records, kMesh 3 with TraceParams::tc_ncells)
+    // (wrecs: the wide walk's records, TraceParams::tw_tris)
     const float4 *recs = wrecs ? wrecs : cam ? p.cam_tris : p.tbvh_tris;
     const uint32_t first = leaf >> 3, end = first + (leaf & 7u);
     tri_done += leaf & 7u;
@@ -1376,7 +1376,7 @@ void trace_kernel(TraceParams p) {
                         lmask &= lmask - 1u;
                         const uint32_t lw = c == 0 ? a[0] : c == 1 ? a[1] : c == 2 ? a[2] : a[3];
                         tri_leaf(p, org, dir, false, lw & ~kLeafBitDev, best_t, tri_t, tri_i, tri_in, tri_done,
-                                 p.tc_ncells != 0u ? p.tw_tris + (size_t)4u * tree * p.tw_rstride : nullptr);
+                                 p.tw_tris);
                     }
                     cap = fminf(best_t, tri_t);
                     uint32_t nxt = 0xFFFFu;

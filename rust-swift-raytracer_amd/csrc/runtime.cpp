@@ -598,11 +598,11 @@ int render_frame(WorldState &w, const CameraModel &cam, size_t width, size_t hei
         if (d->tw_nodes) {
             p.tw_nodes = d->tw_nodes;
             p.tw_depth = d->tw_depth;
+            p.tw_tris = (const float4 *)d->tbvh_tris;
             if (d->tw_tris) {
                 const TriangleCells &tc = w.tcells;
                 p.tw_tris = (const float4 *)d->tw_tris;
                 p.tw_stride = tc.stride_w;
-                p.tw_rstride = tc.stride_r;
                 p.tc_ncells = tc.ncells;
                 for (int k = 0; k < 3; ++k) { p.tc_n[k] = tc.n[k]; p.tc_lo[k] = tc.lo[k]; }
                 p.tc_size = tc.size;
