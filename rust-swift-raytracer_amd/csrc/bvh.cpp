@@ -4,6 +4,7 @@
 #include <algorithm>
 #include <atomic>
 #include <cmath>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <limits>
@@ -640,25 +641,54 @@ float triangle_cell_edge(const std::vector<Triangle> &tris, uint32_t max_cells) 
 }
 
 TriangleCells build_triangle_cells(const std::vector<Triangle> &tris, const std::vector<float> &tri_hot,
-                                   uint32_t leaf_size, float size, TriangleBVH &tb) {
+                                   const std::vector<Sphere> &spheres, uint32_t leaf_size, float size,
+                                   TriangleBVH &tb) {
     TriangleCells out;
     if (tb.nodes.empty() || tb.wnodes.empty() || !(size > 0)) return out;
-    // cells over the box of the mesh's (finite) vertices
+    // The grid covers where secondary rays start near the mesh: the box of the
+    // mesh's (finite) vertices and of every sphere no larger than the mesh
+    // (a ground sphere of radius 1000 would only stretch it; its surface still
+    // marks the cells it crosses below).  RT_AMD_TRI_CELL_SCENE=0: the mesh's
+    // box alone (the first build, A/B only).
     double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+    auto finite3 = [](const Vec3 &v) { return std::isfinite(v.x) && std::isfinite(v.y) && std::isfinite(v.z); };
     for (const Triangle &t : tris)
         for (const Vec3 &v : {t.v0, t.v1, t.v2}) {
+            if (!finite3(v)) continue;
             const double c[3] = {v.x, v.y, v.z};
-            if (!(std::isfinite(c[0]) && std::isfinite(c[1]) && std::isfinite(c[2]))) continue;
             for (int k = 0; k < 3; ++k) { lo[k] = std::min(lo[k], c[k]); hi[k] = std::max(hi[k], c[k]); }
         }
-    uint64_t ncells = 1;
+    double ext = 0;
     for (int k = 0; k < 3; ++k) {
         if (!(lo[k] <= hi[k])) return out;
-        out.lo[k] = (float)lo[k];
-        out.n[k] = (uint32_t)std::max(1.0, std::ceil((hi[k] - out.lo[k]) / size + 1e-9));
-        ncells *= out.n[k];
+        ext = std::max(ext, hi[k] - lo[k]);
     }
-    if (ncells > 4096) return out;
+    const char *scene_env = std::getenv("RT_AMD_TRI_CELL_SCENE");
+    if (!(scene_env && std::atoi(scene_env) == 0))
+        for (const Sphere &sp : spheres) {
+            const double r = std::fabs((double)sp.radius);
+            if (!finite3(sp.center) || !(r <= ext)) continue;
+            const double c[3] = {sp.center.x, sp.center.y, sp.center.z};
+            for (int k = 0; k < 3; ++k) { lo[k] = std::min(lo[k], c[k] - r); hi[k] = std::max(hi[k], c[k] + r); }
+        }
+    // Every cell gets a tree.  (Only cells that a surface passes through
+    // would not do: a triangle's hits lie on its phantom for the ray's origin
+    // (common.rs:141, the sign quirk), so secondary rays start all over the
+    // region around the mesh.  Trees for occupied cells only, 79 of C5's
+    // 189: 106.4 ms; occupancy grown by one cell: 97.7; every cell: 97.7.)
+    // The edge grows until the grid has <= 1024 cells and the trees hold
+    // <= 2e7 triangles in all.
+    uint64_t ncells = 0;
+    for (int attempt = 0; attempt < 64; ++attempt, size *= 1.25f) {
+        ncells = 1;
+        for (int k = 0; k < 3; ++k) {
+            out.lo[k] = (float)lo[k];
+            out.n[k] = (uint32_t)std::max(1.0, std::ceil((hi[k] - out.lo[k]) / size + 1e-9));
+            ncells *= out.n[k];
+        }
+        if (ncells <= 1024 && (double)ncells * (double)tris.size() <= 2e7) break;
+    }
+    if (ncells > 1024 || (double)ncells * (double)tris.size() > 2e7) return TriangleCells{};
     out.size = size;
     out.ncells = (uint32_t)ncells;
     // SAH phantom scale in half-diagonals (RT_AMD_TRI_CELL_SAH, tuning only):
@@ -668,10 +698,8 @@ TriangleCells build_triangle_cells(const std::vector<Triangle> &tris, const std:
     // 0.25 135.1, 0.5 135.3, 1 138.7, 2 145.7, 4 167.8
     const char *sah_env = std::getenv("RT_AMD_TRI_CELL_SAH");
     const double sah = sah_env ? std::max(1e-3, std::atof(sah_env)) : 0.4;
-    // one tree per cell, on host threads.  Every cell gets its own
-    // tree: the kernel widens from the centre of the origin's cell, so a cell's
-    // slot must hold the tree built for that centre (a copy of the static tree
-    // there made frames wrong in a first try)
+    // one tree per cell, on host threads, built for the cell's centre (the
+    // kernel widens from the centre of the origin's cell)
     std::vector<TriangleBVH> trees(ncells);
     std::atomic<uint64_t> next{0};
     auto work = [&]() {

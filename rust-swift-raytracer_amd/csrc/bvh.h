@@ -91,18 +91,19 @@ struct TriangleBVH {
 // Fills tb.wnodes / tb.wdepth from tb.qnodes (build_triangle_bvh calls it).
 void build_wide_image(TriangleBVH &tb);
 
-// Per-origin-cell triangle trees (RT_AMD_TRI_CELLS): the box of
-// the mesh cut into n[0] x n[1] x n[2] cubic cells of edge `size` from `lo`;
-// tree c (c = (z n1 + y) n0 + x) holds the phantoms of origin = its cell's
-// centre (build_triangle_bvh with oc), so a secondary ray whose origin lies in
-// the cell is widened by at most the cell's half-diagonal; tree ncells is the
-// static tree (rays from outside every cell).  Every tree is exact for any
-// origin (the per-ray widening covers o - oc), so the choice of tree only
-// changes the work.  All trees share one quantisation grid (the union of their
-// root boxes; the static tree tb is re-quantised on it), so the kernel's grid
-// parameters stay per launch.  Wide images are concatenated with a fixed
-// stride; the records are one array for all trees (the static tree's, then
-// copies for cell-tree leaves that are not one run of it).
+// Per-origin-cell triangle trees: a grid of cubic cells of
+// edge `size` from `lo` (n[0] x n[1] x n[2], cell c = (z n1 + y) n0 + x) over
+// the box of the mesh and of the spheres no larger than the mesh.  Tree c
+// holds the phantoms of origin = cell c's centre (build_triangle_bvh with oc),
+// so a secondary ray whose origin lies in the cell is widened by at most the
+// cell's half-diagonal; tree ncells is the static tree (origins outside the
+// grid).  Every tree is exact for any origin (the per-ray widening covers
+// o - oc), so the choice of tree only changes the work.  All trees share one
+// quantisation grid (the union of their root boxes; the static tree tb is
+// re-quantised on it), so the kernel's grid parameters stay per launch.  Wide
+// images are concatenated with a fixed stride; the records are one array for
+// all trees (the static tree's, then copies for cell-tree leaves that are not
+// one run of it).
 struct TriangleCells {
     float lo[3] = {0, 0, 0};
     float size = 0;
@@ -114,9 +115,11 @@ struct TriangleCells {
     float mag = 0;                  // largest |coordinate| over the trees (rho)
 };
 // Empty (ncells == 0) when a tree has no wide image or the trees do not fit
-// the kernel's 32-bit indices.
+// the kernel's 32-bit indices.  `size` is the starting edge: it grows until the
+// grid has <= 1024 cells and the trees hold <= 2e7 triangles in all.
 TriangleCells build_triangle_cells(const std::vector<Triangle> &tris, const std::vector<float> &tri_hot,
-                                   uint32_t leaf_size, float size, TriangleBVH &tb);
+                                   const std::vector<Sphere> &spheres, uint32_t leaf_size, float size,
+                                   TriangleBVH &tb);
 // The smallest cell edge (of a geometric ladder) that cuts the box of the
 // mesh's finite vertices into at most max_cells cells; 0 for an empty mesh.
 float triangle_cell_edge(const std::vector<Triangle> &tris, uint32_t max_cells);

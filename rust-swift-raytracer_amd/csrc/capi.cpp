@@ -79,9 +79,11 @@ Rust_WorldHandle *load_world(const char *source) {
                                                   env_leaf("RT_AMD_TRI_LEAF", 1u));
     // per-origin-cell trees: for meshes of >= 64 k triangles
     // by default, cells of the edge that cuts the mesh's box into <= 32 (A/B on
-    // C5, profiles/round6_c5_cells: static tree 147.1 ms; 1.5 / 2 / 2.5-unit cells,
-    // 124 / 56 / 30 trees: 142.5 / 140.0 / 139.5 ms; 3 / 4-unit cells 145.4 /
-    // 149.3 ms); RT_AMD_TRI_CELLS=<edge> sets the edge, 0 switches them off.
+    // C5 over the mesh's box, profiles/round6_c5_cells: static tree 147.1 ms;
+    // 1.5 / 2 / 2.5-unit cells, 124 / 56 / 30 trees: 142.5 / 140.0 / 139.5 ms;
+    // 3 / 4-unit cells 145.4 / 149.3 ms), laid over the box of the mesh and
+    // the spheres around it (bvh.h TriangleCells; C5: 189 trees, 133.1 ->
+    // 97.7 ms); RT_AMD_TRI_CELLS=<edge> sets the edge, 0 switches them off.
     // The static tree is re-quantised on their common grid.
     {
         float size = 0.0f;
@@ -93,11 +95,13 @@ Rust_WorldHandle *load_world(const char *source) {
         if (size > 0.0f)
             world->state.tcells = rtamd::build_triangle_cells(world->state.scene.triangles,
                                                               world->state.packed.tri_hot,
+                                                              world->state.scene.spheres,
                                                               env_leaf("RT_AMD_TRI_LEAF", 1u), size,
                                                               world->state.tbvh);
         const auto &tc = world->state.tcells;
-        if (std::getenv("RT_AMD_TRI_CELLS_DEBUG")) std::fprintf(stderr, "tri cells: %u x %u x %u = %u cells of %.3g, %u wide nodes per tree, %zu records, "
-                     "%.1f MB\n", tc.n[0], tc.n[1], tc.n[2], tc.ncells, tc.size, tc.stride_w, tc.tris.size() / 16,
+        if (std::getenv("RT_AMD_TRI_CELLS_DEBUG")) std::fprintf(stderr, "tri cells: %u x %u x %u = %u cells of %.3g, %u wide nodes per tree, "
+                     "%zu records, %.1f MB\n", tc.n[0], tc.n[1], tc.n[2], tc.ncells, tc.size, tc.stride_w,
+                     tc.tris.size() / 16,
                      (tc.wnodes.size() * 4.0 + tc.tris.size() * 4.0) / 1e6);
     }
     // bounce-0 triangle tree for the scene camera (rebuilt by the first render
