@@ -3,6 +3,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -43,6 +44,10 @@ inline float up(double x) {  // smallest float >= x
     return ((double)f < x) ? std::nextafter(f, std::numeric_limits<float>::infinity()) : f;
 }
 inline float bits_f(uint32_t u) { float f; std::memcpy(&f, &u, 4); return f; }
+
+// set on the threads that build per-cell trees side by side (build_triangle_cells):
+// their builders run serially instead of each starting 16 more threads
+thread_local bool tl_serial_build = false;
 
 struct Builder {
     std::vector<Prim> &prims;
@@ -94,7 +99,7 @@ struct Builder {
         nodes.reserve((size_t)count * 2);
         nodes.emplace_back();
         unsigned hw = std::thread::hardware_concurrency();
-        const unsigned threads = std::min(16u, std::max(1u, hw));
+        const unsigned threads = tl_serial_build ? 1u : std::min(16u, std::max(1u, hw));
         defer = threads > 1 && count >= 4 * kParMin;
         build(0, 0, count, 0);
         defer = false;
@@ -177,8 +182,12 @@ struct Builder {
             scr.lc.resize(kBins);
             Box *bb = scr.bb.data(), *nb = scr.nb.data();
             uint32_t *cnt = scr.cnt.data();
+            // (triangle trees bin with one multiply: the many per-cell builds;
+            // sphere trees keep the division their tuned trees were built with)
+            const double inv = kBins / ext;
             for (uint32_t i = first; i < first + count; ++i) {
-                int b = (int)((key(prims[i], ax) - lo) / ext * kBins);
+                int b = phantom > 0 ? (int)((key(prims[i], ax) - lo) * inv)
+                                    : (int)((key(prims[i], ax) - lo) / ext * kBins);
                 b = std::min(kBins - 1, std::max(0, b));
                 bb[b].grow(prims[i].box);
                 nb[b].grow(prims[i].n);
@@ -222,7 +231,9 @@ struct Builder {
         } else {
             auto it = std::partition(prims.begin() + first, prims.begin() + first + count,
                                      [&](const Prim &p) {
-                                         int b = (int)((key(p, best_axis) - best_lo) / best_ext * kBins);
+                                         int b = phantom > 0
+                                                     ? (int)((key(p, best_axis) - best_lo) * (kBins / best_ext))
+                                                     : (int)((key(p, best_axis) - best_lo) / best_ext * kBins);
                                          b = std::min(kBins - 1, std::max(0, b));
                                          return b < best_split;
                                      });
@@ -441,7 +452,7 @@ static void quantize_boxes(const std::vector<float> &nodes, size_t stride, bool 
 }
 
 TriangleBVH build_triangle_bvh(const std::vector<Triangle> &tris, const std::vector<float> &tri_hot,
-                               uint32_t leaf_size, const float *oc, double phantom) {
+                               uint32_t leaf_size, const float *oc, double phantom, bool image) {
     TriangleBVH out;
     if (oc)
         for (int k = 0; k < 3; ++k) out.oc[k] = oc[k];
@@ -518,8 +529,10 @@ TriangleBVH build_triangle_bvh(const std::vector<Triangle> &tris, const std::vec
     out.miss.assign(b.nodes.size() * 8, kNodeEnd);
     for (uint32_t oct = 0; oct < 8; ++oct) b.links(0, kNodeEnd, oct, out.miss);
     out.tris = triangle_records(prims, tris, tri_hot);
-    quantize_boxes(out.nodes, 16, true, out.miss, out.qnodes, out.qbox, &out.nbase, &out.nstep);
-    build_wide_image(out);
+    if (image) {
+        quantize_boxes(out.nodes, 16, true, out.miss, out.qnodes, out.qbox, &out.nbase, &out.nstep);
+        build_wide_image(out);
+    }
     return out;
 }
 
@@ -676,19 +689,23 @@ TriangleCells build_triangle_cells(const std::vector<Triangle> &tris, const std:
     // (common.rs:141, the sign quirk), so secondary rays start all over the
     // region around the mesh.  Trees for occupied cells only, 79 of C5's
     // 189: 106.4 ms; occupancy grown by one cell: 97.7; every cell: 97.7.)
-    // The edge grows until the grid has <= 1024 cells and the trees hold
-    // <= 2e7 triangles in all.
+    // The edge grows (5 % steps) until the grid has <= 1024 cells and the
+    // trees hold <= 4e7 triangles in all (C5, 2.49 / 2.2 / 2.0-unit cells:
+    // 189 / 320 / 396 trees, 97.2 / 91.1 / 88.7 ms).
+    // (RT_AMD_TRI_CELL_BUDGET: the triangle budget, tuning only)
+    const char *budget_env = std::getenv("RT_AMD_TRI_CELL_BUDGET");
+    const double budget = budget_env ? std::atof(budget_env) : 4e7;
     uint64_t ncells = 0;
-    for (int attempt = 0; attempt < 64; ++attempt, size *= 1.25f) {
+    for (int attempt = 0; attempt < 400; ++attempt, size *= 1.05f) {
         ncells = 1;
         for (int k = 0; k < 3; ++k) {
             out.lo[k] = (float)lo[k];
             out.n[k] = (uint32_t)std::max(1.0, std::ceil((hi[k] - out.lo[k]) / size + 1e-9));
             ncells *= out.n[k];
         }
-        if (ncells <= 1024 && (double)ncells * (double)tris.size() <= 2e7) break;
+        if (ncells <= 1024 && (double)ncells * (double)tris.size() <= budget) break;
     }
-    if (ncells > 1024 || (double)ncells * (double)tris.size() > 2e7) return TriangleCells{};
+    if (ncells > 1024 || (double)ncells * (double)tris.size() > budget) return TriangleCells{};
     out.size = size;
     out.ncells = (uint32_t)ncells;
     // SAH phantom scale in half-diagonals (RT_AMD_TRI_CELL_SAH, tuning only):
@@ -703,32 +720,51 @@ TriangleCells build_triangle_cells(const std::vector<Triangle> &tris, const std:
     std::vector<TriangleBVH> trees(ncells);
     std::atomic<uint64_t> next{0};
     auto work = [&]() {
+        tl_serial_build = true;
         for (uint64_t c; (c = next++) < ncells;) {
             const uint64_t x = c % out.n[0], y = (c / out.n[0]) % out.n[1], z = c / (out.n[0] * out.n[1]);
             const float oc[3] = {out.lo[0] + ((float)x + 0.5f) * size, out.lo[1] + ((float)y + 0.5f) * size,
                                  out.lo[2] + ((float)z + 0.5f) * size};
-            trees[c] = build_triangle_bvh(tris, tri_hot, leaf_size, oc, size * 0.866 * sah);
+            trees[c] = build_triangle_bvh(tris, tri_hot, leaf_size, oc, size * 0.866 * sah, false);
         }
     };
     const unsigned nt = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    const auto t0 = std::chrono::steady_clock::now();
     std::vector<std::thread> pool;
     for (unsigned i = 1; i < nt; ++i) pool.emplace_back(work);
     work();
     for (auto &t : pool) t.join();
+    const auto t1 = std::chrono::steady_clock::now();
     // one grid for every tree (and the static one): the union of their roots
     float glo[3], ghi[3];
     for (int k = 0; k < 3; ++k) { glo[k] = tb.nodes[k]; ghi[k] = tb.nodes[4 + k]; }
     for (uint64_t c = 0; c < ncells; ++c) {
         const TriangleBVH &t = trees[c];
-        if (t.nodes.empty() || t.wnodes.empty()) return TriangleCells{};
+        if (t.nodes.empty()) return TriangleCells{};
         for (int k = 0; k < 3; ++k) { glo[k] = std::min(glo[k], t.nodes[k]); ghi[k] = std::max(ghi[k], t.nodes[4 + k]); }
     }
     trees.push_back(tb);
+    {  // every tree (and the static one) on the common grid, on the same threads
+        std::atomic<uint64_t> next_q{0};
+        auto quant = [&]() {
+            for (uint64_t c; (c = next_q++) <= ncells;) {
+                TriangleBVH &t = trees[c];
+                quantize_boxes(t.nodes, 16, true, t.miss, t.qnodes, t.qbox, &t.nbase, &t.nstep, glo, ghi);
+                build_wide_image(t);
+            }
+        };
+        std::vector<std::thread> qpool;
+        for (unsigned i = 1; i < nt; ++i) qpool.emplace_back(quant);
+        quant();
+        for (auto &t : qpool) t.join();
+    }
+    const auto t2 = std::chrono::steady_clock::now();
+    if (std::getenv("RT_AMD_TRI_CELLS_DEBUG"))
+        std::fprintf(stderr, "cell trees: build %.2f s, quantise + wide images %.2f s\n",
+                     std::chrono::duration<double>(t1 - t0).count(), std::chrono::duration<double>(t2 - t1).count());
     uint64_t sw = 0;
     for (uint64_t c = 0; c <= ncells; ++c) {
         TriangleBVH &t = trees[c];
-        quantize_boxes(t.nodes, 16, true, t.miss, t.qnodes, t.qbox, &t.nbase, &t.nstep, glo, ghi);
-        build_wide_image(t);
         if (t.wnodes.empty()) return TriangleCells{};
         sw = std::max<uint64_t>(sw, t.wnodes.size() / 32);
         out.wdepth = std::max(out.wdepth, t.wdepth);

@@ -116,7 +116,7 @@ struct TriangleCells {
 };
 // Empty (ncells == 0) when a tree has no wide image or the trees do not fit
 // the kernel's 32-bit indices.  `size` is the starting edge: it grows until the
-// grid has <= 1024 cells and the trees hold <= 2e7 triangles in all.
+// grid has <= 1024 cells and the trees hold <= 4e7 triangles in all.
 TriangleCells build_triangle_cells(const std::vector<Triangle> &tris, const std::vector<float> &tri_hot,
                                    const std::vector<Sphere> &spheres, uint32_t leaf_size, float size,
                                    TriangleBVH &tb);
@@ -126,10 +126,11 @@ float triangle_cell_edge(const std::vector<Triangle> &tris, uint32_t max_cells);
 
 // tri_hot: PackedScene::tri_hot (the exact per-triangle n and n.v0 bits).
 // oc (optional): origin the boxes are built for; phantom: SAH weight of the
-// normal spread (<= 0: derived from the scene).
+// normal spread (<= 0: derived from the scene); image = false: no quantised
+// nodes and wide image (build_triangle_cells makes them on its common grid).
 TriangleBVH build_triangle_bvh(const std::vector<Triangle> &tris, const std::vector<float> &tri_hot,
                                uint32_t leaf_size, const float *oc = nullptr,
-                               double phantom = 0);
+                               double phantom = 0, bool image = true);
 
 // Primary rays all start at the camera origin, so their phantom triangles are
 // fixed: this tree holds, per triangle of `tb`, its box translated by

@@ -78,19 +78,18 @@ Rust_WorldHandle *load_world(const char *source) {
                                                   world->state.packed.tri_hot,
                                                   env_leaf("RT_AMD_TRI_LEAF", 1u));
     // per-origin-cell trees: for meshes of >= 64 k triangles
-    // by default, cells of the edge that cuts the mesh's box into <= 32 (A/B on
-    // C5 over the mesh's box, profiles/round6_c5_cells: static tree 147.1 ms;
-    // 1.5 / 2 / 2.5-unit cells, 124 / 56 / 30 trees: 142.5 / 140.0 / 139.5 ms;
-    // 3 / 4-unit cells 145.4 / 149.3 ms), laid over the box of the mesh and
-    // the spheres around it (bvh.h TriangleCells; C5: 189 trees, 133.1 ->
-    // 97.7 ms); RT_AMD_TRI_CELLS=<edge> sets the edge, 0 switches them off.
-    // The static tree is re-quantised on their common grid.
+    // by default, over the box of the mesh and the spheres around it, starting
+    // from the edge that cuts the mesh's box into <= 1024 cells and grown to the
+    // trees' budget (bvh.h TriangleCells; C5: 396 trees of 2-unit cells, static
+    // tree 143.6 ms -> 88.7 ms); RT_AMD_TRI_CELLS=<edge> sets the starting
+    // edge, 0 switches them off.  The static tree is re-quantised on their
+    // common grid.
     {
         float size = 0.0f;
         if (const char *cs = std::getenv("RT_AMD_TRI_CELLS")) {
             size = std::strtof(cs, nullptr);
         } else if (world->state.scene.triangles.size() >= 65536 && !world->state.tbvh.nodes.empty()) {
-            size = rtamd::triangle_cell_edge(world->state.scene.triangles, 32);
+            size = rtamd::triangle_cell_edge(world->state.scene.triangles, 1024);
         }
         if (size > 0.0f)
             world->state.tcells = rtamd::build_triangle_cells(world->state.scene.triangles,
