@@ -8,7 +8,9 @@
 //   * quantised kernel nodes decode (fmaf(q, step, base)) to boxes containing
 //     the float boxes, and the packed child/axis/leaf words round-trip.
 // Prints "OK <counts>" or the first failure and exits non-zero.
+#include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <map>
@@ -182,6 +184,74 @@ static void check_wide(const TriangleBVH &tb) {
     CHECK(leaves.size() == nleaf, "wide: %zu leaf words, %zu binary leaves\n", leaves.size(), nleaf);
 }
 
+// Per-origin-cell trees (bvh.h TriangleCells, argv[3] = starting cell edge):
+// the grid covers the mesh and the spheres no larger than it, the image holds
+// ncells + 1 trees of stride_w wide nodes with the static tree last (equal to
+// the re-quantised tb), the records begin with the static tree's, and every
+// tree's walk reaches each of its wide nodes once and each tree triangle in
+// exactly one leaf.
+static void check_cells(const SceneModel &s, const TriangleCells &tc, const TriangleBVH &tb) {
+    CHECK(tc.ncells == tc.n[0] * tc.n[1] * tc.n[2] && tc.ncells > 0, "cells: %u != grid\n", tc.ncells);
+    CHECK(tc.ncells <= 1024, "cells: %u > 1024\n", tc.ncells);
+    const size_t sw = tc.stride_w;
+    CHECK(tc.wnodes.size() == (size_t)(tc.ncells + 1) * sw * 32, "cells: image size\n");
+    double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY}, ext = 0;
+    for (const Triangle &t : s.triangles)
+        for (const Vec3 &v : {t.v0, t.v1, t.v2}) {
+            const double c[3] = {v.x, v.y, v.z};
+            for (int k = 0; k < 3; ++k) { lo[k] = std::min(lo[k], c[k]); hi[k] = std::max(hi[k], c[k]); }
+        }
+    for (int k = 0; k < 3; ++k) ext = std::max(ext, hi[k] - lo[k]);
+    for (const Sphere &sp : s.spheres) {
+        const double r = std::fabs((double)sp.radius), c[3] = {sp.center.x, sp.center.y, sp.center.z};
+        if (!(r <= ext)) continue;
+        for (int k = 0; k < 3; ++k) { lo[k] = std::min(lo[k], c[k] - r); hi[k] = std::max(hi[k], c[k] + r); }
+    }
+    for (int k = 0; k < 3; ++k)
+        CHECK(tc.lo[k] <= lo[k] + 1e-6 * (1 + std::fabs(lo[k])) && tc.lo[k] + (double)tc.n[k] * tc.size >= hi[k] - 1e-4,
+              "cells: axis %d [%g, %g] not covered\n", k, lo[k], hi[k]);
+    CHECK(std::equal(tb.wnodes.begin(), tb.wnodes.end(), tc.wnodes.begin() + (size_t)tc.ncells * sw * 32),
+          "cells: static slot differs from tb\n");
+    CHECK(tc.tris.size() >= tb.tris.size() && std::equal(tb.tris.begin(), tb.tris.end(), tc.tris.begin()),
+          "cells: records do not begin with the static tree's\n");
+    std::vector<int> want(s.triangles.size(), 0);
+    for (size_t j = 0; j < tb.tris.size() / 16; ++j) {
+        uint32_t id;
+        std::memcpy(&id, &tb.tris[j * 16 + 7], 4);
+        want[id]++;
+    }
+    for (uint32_t c = 0; c <= tc.ncells; ++c) {
+        const uint32_t *img = &tc.wnodes[(size_t)c * sw * 32];
+        std::vector<int> seen(sw, 0), got(s.triangles.size(), 0);
+        std::vector<uint32_t> st{0u};
+        while (!st.empty()) {
+            const uint32_t w = st.back();
+            st.pop_back();
+            CHECK(w < sw, "cells: tree %u node %u out of range\n", c, w);
+            if (w >= sw) return;
+            seen[w]++;
+            for (int k = 0; k < 4; ++k) {
+                const uint32_t a = img[(size_t)w * 32 + 24 + k];
+                if (!(a & kLeafBit)) { st.push_back(a); continue; }
+                const uint32_t first = (a & ~kLeafBit) >> 3, count = a & 7u;
+                CHECK((size_t)(first + count) * 16 <= tc.tris.size(), "cells: tree %u leaf past records\n", c);
+                for (uint32_t j = first; j < first + count && (size_t)(j + 1) * 16 <= tc.tris.size(); ++j) {
+                    uint32_t id;
+                    std::memcpy(&id, &tc.tris[(size_t)j * 16 + 7], 4);
+                    if (id < got.size()) got[id]++;
+                }
+            }
+        }
+        size_t nreached = 0;
+        for (size_t w = 0; w < sw; ++w) {
+            CHECK(seen[w] <= 1, "cells: tree %u node %zu reached %d times\n", c, w, seen[w]);
+            nreached += seen[w];
+        }
+        CHECK(got == want, "cells: tree %u does not hold every tree triangle once\n", c);
+        if (fails) return;
+    }
+}
+
 int main(int argc, char **argv) {
     std::ifstream fh(argv[1]);
     std::stringstream ss;
@@ -220,6 +290,16 @@ int main(int argc, char **argv) {
         CHECK(in_tree + tb.loose.size() + degenerate >= s.triangles.size(),
               "triangles lost: %zu tree + %zu loose + %zu degenerate < %zu\n", in_tree, tb.loose.size(),
               degenerate, s.triangles.size());
+    size_t ncells = 0;
+    if (argc > 3 && !tb.nodes.empty()) {
+        TriangleBVH tb2 = tb;
+        const TriangleCells tc = build_triangle_cells(s.triangles, p.tri_hot, s.spheres, leaf,
+                                                      (float)std::atof(argv[3]), tb2);
+        ncells = tc.ncells;
+        if (ncells) check_cells(s, tc, tb2);
+        else CHECK(false, "cells: none built\n");
+        std::printf("cells %zu\n", ncells);
+    }
     if (fails) return 1;
     std::printf("OK spheres %zu nodes %zu | triangles %zu tree %zu loose %zu nodes %zu camera nodes %zu\n",
                 s.spheres.size(), sb.nodes.size() / 8, s.triangles.size(), in_tree, tb.loose.size(),

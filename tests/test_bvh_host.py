@@ -24,10 +24,11 @@ def checker(tmp_path_factory):
     return exe
 
 
-def run(checker, tmp_path, text, leaf=2):
+def run(checker, tmp_path, text, leaf=2, cells=None):
     path = tmp_path / "scene.txt"
     path.write_text(text)
-    r = subprocess.run([checker, str(path), str(leaf)], capture_output=True, text=True)
+    args = [checker, str(path), str(leaf)] + ([str(cells)] if cells is not None else [])
+    r = subprocess.run(args, capture_output=True, text=True)
     assert r.returncode == 0, r.stdout + r.stderr
     return r.stdout
 
@@ -47,6 +48,21 @@ def test_rtow_sphere_tree(checker, tmp_path):
 def test_triangle_trees(checker, tmp_path, case, leaf):
     out = run(checker, tmp_path, S.triangle_soup(**case), leaf)
     assert "OK" in out
+
+
+@pytest.mark.parametrize("case,edge", [
+    (dict(seed=13, n=300, spheres=200, grid=12), 1.3),
+    (dict(seed=12, n=400, size=2.0, dup=80, slivers=30), 2.5),
+    (dict(seed=14, n=500, big=6, spread=8.0), 0.2),   # grows to the 1,024-cell cap
+])
+def test_triangle_cell_trees_structure(checker, tmp_path, case, edge):
+    """Per-origin-cell trees (bvh.h TriangleCells): the grid covers the mesh
+    and the spheres no larger than it, every tree (and the static one, last)
+    holds each tree triangle in exactly one leaf of the shared record array."""
+    out = run(checker, tmp_path, S.triangle_soup(**case), 1, cells=edge)
+    assert "OK" in out
+    ncells = int(out.split("cells ")[1].split()[0])
+    assert 0 < ncells <= 1024
 
 
 def test_mesh_c5_trees(checker, tmp_path):
