@@ -751,6 +751,11 @@ TriangleCells build_triangle_cells(const std::vector<Triangle> &tris, const std:
                 TriangleBVH &t = trees[c];
                 quantize_boxes(t.nodes, 16, true, t.miss, t.qnodes, t.qbox, &t.nbase, &t.nstep, glo, ghi);
                 build_wide_image(t);
+                if (c < ncells) {  // a cell tree keeps only its wide image and records (host memory)
+                    std::vector<float>().swap(t.nodes);
+                    std::vector<uint32_t>().swap(t.miss);
+                    std::vector<uint32_t>().swap(t.qnodes);
+                }
             }
         };
         std::vector<std::thread> qpool;
