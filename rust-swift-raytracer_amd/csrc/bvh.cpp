@@ -720,6 +720,7 @@ TriangleCells build_triangle_cells(const std::vector<Triangle> &tris, const std:
     std::vector<TriangleBVH> trees(ncells);
     std::atomic<uint64_t> next{0};
     auto work = [&]() {
+        const bool was_serial = tl_serial_build;  // (the calling thread runs work() too)
         tl_serial_build = true;
         for (uint64_t c; (c = next++) < ncells;) {
             const uint64_t x = c % out.n[0], y = (c / out.n[0]) % out.n[1], z = c / (out.n[0] * out.n[1]);
@@ -727,6 +728,7 @@ TriangleCells build_triangle_cells(const std::vector<Triangle> &tris, const std:
                                  out.lo[2] + ((float)z + 0.5f) * size};
             trees[c] = build_triangle_bvh(tris, tri_hot, leaf_size, oc, size * 0.866 * sah, false);
         }
+        tl_serial_build = was_serial;
     };
     const unsigned nt = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
     const auto t0 = std::chrono::steady_clock::now();
